@@ -1,0 +1,191 @@
+#!/usr/bin/env python3
+"""bench.py — particle-updates/s of the per-particle step on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[2]): 1e8 particles per GPU, 4 attractors
+moving on circles, drag, lifetime decay + Philox respawn, semi-implicit Euler, walls.  One
+"step" = one fused stream-kernel launch over every particle (in place, SoA, 40 B/particle
+of algorithmic HBM traffic).  Multi-GPU: one process per GPU, contiguous index shards with
+global particle ids, no data-path collective (weak scaling: 1e8 particles per rank).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Prints ONE JSON line on rank 0 (fields: see the contract in DESIGN.md §6).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "rust-particle-system_amd", "python"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+METRIC = "particle-updates/sec + achieved HBM GB/s, 10^8 particles, 1/2/4/8 MI355X"
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--particles", type=int, default=100_000_000, help="particles per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget")
+    ap.add_argument("--cpu-sample", type=int, default=1 << 22, help="CPU-baseline particles")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--seed", type=int, default=0x5EED)
+    return ap.parse_args()
+
+
+class Dist:
+    """torch.distributed when launched by torchrun; a no-op single process otherwise."""
+
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dist = None
+        if "RANK" in os.environ and "WORLD_SIZE" in os.environ:
+            import torch  # imported before librps so both share torch's HIP runtime
+            import torch.distributed as dist
+
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            if backend == "nccl":
+                torch.cuda.set_device(self.local)
+            dist.init_process_group(backend=backend)
+            self.torch, self.dist, self.backend = torch, dist, backend
+
+    def barrier(self):
+        if self.dist:
+            if self.backend == "nccl":
+                self.dist.barrier(device_ids=[self.local])
+            else:
+                self.dist.barrier()
+
+    def sync_device(self):
+        if self.dist and self.backend == "nccl":
+            self.torch.cuda.synchronize()
+
+    def max(self, v: float) -> float:
+        if not self.dist:
+            return v
+        dev = f"cuda:{self.local}" if self.backend == "nccl" else "cpu"
+        t = self.torch.tensor([v], dtype=self.torch.float64, device=dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def workload(rps, n_rank, world):
+    cfg = rps.default_particle_config(min(n_rank * world, 0xFFFFFFFF), gravity=0.0)
+    ext = rps.headline_ext(stats=True)  # stats reduced every 100 steps (amortised)
+    ext.shader_delay = 0  # every timed step is an active step
+    return cfg, ext
+
+
+def pmc_traffic(workload_name):
+    try:
+        with open(PMC_FILE) as f:
+            d = json.load(f)
+        return d.get(workload_name, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(rps, args, cfg, ext):
+    """The oracle's OpenMP build (same f32 semantics as the kernel) on the host cores, on a
+    bounded sample of the workload: the same per-particle step over `cpu_sample` particles
+    with the C3 configuration, repeated for about `cpu_seconds`."""
+    import oracle as orc
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    n = args.cpu_sample
+    soa = orc.init_scatter(cfg, ext, args.seed, n, global_count=args.particles)
+    orc.stream_step_omp(cfg, ext, soa, 0, threads=threads)  # warm (page-in, thread pool)
+    t0 = time.perf_counter()
+    steps = 0
+    while True:
+        orc.stream_step_omp(cfg, ext, soa, 1 + steps, threads=threads)
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds or steps >= 10000:
+            break
+    return {"value": n * steps / el, "unit": "particle-updates/s", "cores": threads, "kind": "port",
+            "sample": f"{n} particles x {steps} steps of the C3 step (oracle/rps_oracle.c, -O3 -fopenmp, "
+                      f"{threads} threads), {el:.1f} s"}
+
+
+def main():
+    args = parse()
+    d = Dist()
+    import rps_amd as rps
+
+    n = args.particles
+    cfg, ext = workload(rps, n, d.world)
+    wl = "C3-1e8-4att-drag-respawn-euler"
+    ctx = rps.Context(n, rps.MODE_STREAM, device=d.local if d.dist else 0,
+                      id_offset=d.rank * n, global_count=d.world * n)
+    ctx.set_config(cfg, ext)
+    ctx.init_scatter(args.seed)
+    ctx.step(args.warmup)
+    ctx.sync()
+
+    d.sync_device()
+    d.barrier()
+    ctx.set_profiling(True)
+    t0 = time.perf_counter()
+    ctx.step(args.steps)
+    ctx.sync()
+    d.sync_device()
+    t1 = time.perf_counter()
+    d.barrier()
+    elapsed = d.max(t1 - t0)
+    kern_ms, launches = ctx.kernel_time()
+    kern_ms = d.max(kern_ms)
+    bytes_per_launch, _ = ctx.step_cost()
+    st = ctx.stats()
+    ctx.close()
+
+    updates = float(n) * d.world * args.steps
+    value = updates / elapsed
+    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+    hbm_wall = bytes_per_launch * args.steps / elapsed / 1e9  # per GPU, wall clock incl. gaps
+    traffic = pmc_traffic(wl)
+    line = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "particle-updates/s",
+        "n_gpus": d.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded device scatter of src/main.rs:182-216; Philox respawn)",
+        "config": {"workload": wl, "particles_per_gpu": n, "global_particles": n * d.world,
+                   "attractors": 4, "drag": 0.1, "lifetime_s": [1.0, 5.0], "integrator": "euler",
+                   "bytes_per_particle_step": bytes_per_launch / n, "parallelism": f"index-shard x{d.world}"},
+        "hbm_gbps_per_gpu": hbm_wall,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBPS,
+                     "traffic": traffic, "kernel": "stream_step_kernel<euler,lifetime>",
+                     "avg_kernel_ms": kern_ms, "launches": launches},
+        "stats": {"bbox": list(st.bbox), "respawned_last": st.respawned, "particles": st.particles},
+    }
+    if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(rps, args, cfg, ext)
+    if d.rank == 0:
+        print(json.dumps(line), flush=True)
+    d.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,204 @@
+"""ctypes wrapper of the CPU oracle (oracle/rps_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg — as the checker or the timed CPU baseline, never as the product path.
+PARITY UNPINNED at the WGSL-execution boundary (see rps_oracle.h and DESIGN.md §7).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_BUILD = os.path.join(_HERE, "_build")
+_libs = {}
+
+_P, _U32, _U64, _I, _F = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, ctypes.c_float
+
+
+class OrcStats(ctypes.Structure):
+    _fields_ = [("bbox", ctypes.c_float * 4), ("kinetic_energy", ctypes.c_double),
+                ("particles", ctypes.c_uint64), ("respawned", ctypes.c_uint64)]
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib(omp: bool = False) -> ctypes.CDLL:
+    name = "librps_oracle_omp.so" if omp else "librps_oracle.so"
+    if name in _libs:
+        return _libs[name]
+    path = os.path.join(_BUILD, name)
+    if not os.path.exists(path):
+        build()
+    L = ctypes.CDLL(path)
+    sig = {
+        "orc_philox4x32_10": (None, [_P, _P, _P]),
+        "orc_sincos_turns": (None, [_F, ctypes.POINTER(_F), ctypes.POINTER(_F)]),
+        "orc_attractor_pos": (None, [_P, ctypes.c_double, ctypes.POINTER(_F), ctypes.POINTER(_F)]),
+        "orc_set_color": (None, [_F, _F, _F, _P]),
+        "orc_hash_cell": (_U32, [ctypes.c_int32, ctypes.c_int32]),
+        "orc_cell_key": (_U32, [ctypes.c_int32, ctypes.c_int32, _U32]),
+        "orc_f32_to_i32": (ctypes.c_int32, [_F]),
+        "orc_stream_step": (None, [_P, _P, _U64, _U64, _P, _P, _P, _P, _P, _U64, _P]),
+        "orc_stream_step_omp": (None, [_P, _P, _U64, _U64, _P, _P, _P, _P, _P, _U64, _I]),
+        "orc_init_scatter": (None, [_P, _P, _U64, _U64, _U64, _P, _P, _P, _P, _P, _U64]),
+        "orc_nbody_accel": (None, [_P, _P, _P, _U64, _U64, _U64, _P, _P]),
+        "orc_nbody_integrate": (None, [_P, _P, _P, _P, _P, _P, _P, _P, _U64]),
+        "orc_sph_bin": (None, [_P, _P, _P, _P, _P, _U32]),
+        "orc_sph_sort": (_U32, [_P, _U32]),
+        "orc_sph_offsets": (None, [_P, _P, _U32]),
+        "orc_sph_pre": (None, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _U32]),
+        "orc_sph_sim": (None, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _U32]),
+    }
+    for k, (res, args) in sig.items():
+        f = getattr(L, k)
+        f.restype = res
+        f.argtypes = args
+    _libs[name] = L
+    return L
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _ref(s):
+    return ctypes.cast(ctypes.byref(s), ctypes.c_void_p)
+
+
+def philox(ctr, key):
+    C = np.asarray(ctr, dtype=np.uint32)
+    K = np.asarray(key, dtype=np.uint32)
+    O = np.zeros(4, dtype=np.uint32)
+    lib().orc_philox4x32_10(_p(C), _p(K), _p(O))
+    return O
+
+
+def sincos_turns(u):
+    c, s = ctypes.c_float(), ctypes.c_float()
+    lib().orc_sincos_turns(u, ctypes.byref(c), ctypes.byref(s))
+    return c.value, s.value
+
+
+def set_color(vx, vy, max_energy):
+    out = np.zeros(4, dtype=np.float32)
+    lib().orc_set_color(vx, vy, max_energy, _p(out))
+    return out
+
+
+def set_color_array(vx, vy, max_energy):
+    """Vectorised set_color restatement (same f32 ops) for whole arrays."""
+    vx = np.asarray(vx, np.float32)
+    vy = np.asarray(vy, np.float32)
+    speed_sq = vx * vx + vy * vy
+    energy = np.float32(0.5) * speed_sq
+    with np.errstate(divide="ignore", invalid="ignore"):
+        nrm = energy / np.float32(max_energy)
+    nrm = np.where(nrm < 0, np.float32(0), nrm)
+    nrm = np.where(nrm > 1, np.float32(1), nrm).astype(np.float32)
+    lo = nrm < np.float32(0.5)
+    t_lo = nrm * np.float32(2.0)
+    t_hi = (nrm - np.float32(0.5)) * np.float32(2.0)
+    out = np.zeros((len(vx), 4), np.float32)
+    out[:, 0] = np.where(lo, np.float32(0), t_hi)
+    out[:, 1] = np.where(lo, t_lo, np.float32(1) - t_hi)
+    out[:, 2] = np.where(lo, np.float32(1) - t_lo, np.float32(0))
+    out[:, 3] = 1.0
+    return out
+
+
+def stream_step(cfg, ext, soa, active_step, id_offset=0, stats=False):
+    """One active stream step in place on soa = dict(x, y, vx, vy[, life]) float32 arrays."""
+    life = soa.get("life")
+    use_life = life is not None and (ext.flags & 1)
+    st = OrcStats() if stats else None
+    lib().orc_stream_step(_ref(cfg), _ref(ext), id_offset, active_step, _p(soa["x"]), _p(soa["y"]),
+                          _p(soa["vx"]), _p(soa["vy"]), _p(life) if use_life else None,
+                          len(soa["x"]), _ref(st) if st is not None else None)
+    return st
+
+
+def stream_step_omp(cfg, ext, soa, active_step, id_offset=0, threads=0):
+    life = soa.get("life")
+    use_life = life is not None and (ext.flags & 1)
+    lib(omp=True).orc_stream_step_omp(_ref(cfg), _ref(ext), id_offset, active_step, _p(soa["x"]),
+                                      _p(soa["y"]), _p(soa["vx"]), _p(soa["vy"]),
+                                      _p(life) if use_life else None, len(soa["x"]), threads)
+
+
+def init_scatter(cfg, ext, seed, n, id_offset=0, global_count=None, life=True):
+    global_count = global_count or (id_offset + n)
+    soa = {k: np.zeros(n, np.float32) for k in ("x", "y", "vx", "vy")}
+    soa["life"] = np.zeros(n, np.float32) if life else None
+    lib().orc_init_scatter(_ref(cfg), _ref(ext), seed, id_offset, global_count, _p(soa["x"]),
+                           _p(soa["y"]), _p(soa["vx"]), _p(soa["vy"]), _p(soa["life"]), n)
+    return soa
+
+
+def nbody_accel(ext, sx, sy, t0=0, nt=None):
+    sx = np.ascontiguousarray(sx, np.float32)
+    sy = np.ascontiguousarray(sy, np.float32)
+    nt = len(sx) - t0 if nt is None else nt
+    ax = np.zeros(nt, np.float32)
+    ay = np.zeros(nt, np.float32)
+    lib().orc_nbody_accel(_ref(ext), _p(sx), _p(sy), len(sx), t0, nt, _p(ax), _p(ay))
+    return ax, ay
+
+
+def nbody_integrate(cfg, ext, ax, ay, soa):
+    lib().orc_nbody_integrate(_ref(cfg), _ref(ext), _p(ax), _p(ay), _p(soa["x"]), _p(soa["y"]),
+                              _p(soa["vx"]), _p(soa["vy"]), len(soa["x"]))
+
+
+class SphState:
+    """Host buffers of the reference's SPH path (src/particle_buffers.rs:84-168)."""
+
+    def __init__(self, n):
+        self.n = n
+        p = 1
+        while p < n:
+            p <<= 1
+        self.P = p
+        self.lookup = np.zeros(2 * p, np.uint32)  # zero-initialised like the wgpu buffer
+        self.offsets = np.zeros(n, np.uint32)
+        self.dens = np.zeros(2 * n, np.float32)
+        self.pred = np.zeros(2 * n, np.float32)
+
+    def grid(self, cfg, soa):
+        L = lib()
+        L.orc_sph_bin(_ref(cfg), _p(soa["x"]), _p(soa["y"]), _p(self.lookup), _p(self.offsets), self.n)
+        passes = L.orc_sph_sort(_p(self.lookup), self.n)
+        L.orc_sph_offsets(_p(self.lookup), _p(self.offsets), self.n)
+        return passes
+
+    def pre(self, cfg, soa):
+        lib().orc_sph_pre(_ref(cfg), _p(soa["vx"]), _p(soa["vy"]), _p(soa["x"]), _p(soa["y"]),
+                          _p(self.lookup), _p(self.offsets), _p(self.dens), _p(self.pred), self.n)
+
+    def sim(self, cfg, soa):
+        lib().orc_sph_sim(_ref(cfg), _p(soa["x"]), _p(soa["y"]), _p(soa["vx"]), _p(soa["vy"]),
+                          _p(self.lookup), _p(self.offsets), _p(self.dens), _p(self.pred), self.n)
+
+
+def run_steps(mode, cfg, ext, soa, nsteps, frame_count=0, active_steps=0, id_offset=0, sph=None):
+    """rps_step semantics on the CPU: frame_count += 1 per step (particle_buffers.rs:227),
+    passes gated by frame_count < shader_delay (wgsl:426/:442).  Returns counters."""
+    for _ in range(nsteps):
+        frame_count += 1
+        active = frame_count >= ext.shader_delay
+        if mode == 2:
+            cfg.frame_count = frame_count
+            sph.grid(cfg, soa)
+            if active:
+                sph.pre(cfg, soa)
+                sph.sim(cfg, soa)
+        elif active:
+            stream_step(cfg, ext, soa, active_steps, id_offset)
+        if active:
+            active_steps += 1
+    return frame_count, active_steps

@@ -1,0 +1,88 @@
+/*
+ * rps_oracle.h — CPU restatement of the reference's per-particle step.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library, and only as the checker / the timed CPU
+ * baseline — never as the product path (librps.so has no dependency on it).
+ *
+ * PARITY UNPINNED at the WGSL-execution boundary: the reference (Rust + Bevy 0.16.1 +
+ * wgpu 24.0.5, Cargo.lock:318/:4464) cannot be built or run in this pipeline and ships no
+ * tests, fixtures or golden vectors.  This file restates
+ * assets/compute_shader.wgsl operation by operation (each function cites the line it
+ * follows) with IEEE binary32 arithmetic, no FMA contraction (-ffp-contract=off),
+ * correctly-rounded division and sqrt, and snapshot semantics where the WGSL races
+ * (DESIGN.md §3.3).  What *is* pinned: the known-answer values of tests/golden/ (kernel
+ * norms, hash keys, bitonic pass counts, Random123 Philox KATs) computed independently.
+ */
+#ifndef RPS_ORACLE_H_
+#define RPS_ORACLE_H_
+
+#include <stdint.h>
+#include "../include/rps.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct orc_stats {
+  float bbox[4];
+  double kinetic_energy;
+  uint64_t particles;
+  uint64_t respawned;
+} orc_stats;
+
+/* Random123 Philox4x32-10. */
+void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+/* Deterministic polynomial sin/cos of 2*pi*u, u in [0,1). */
+void orc_sincos_turns(float u, float* c, float* s);
+/* Attractor k position at time t (double precision, rounded to float). */
+void orc_attractor_pos(const rps_attractor* a, double t, float* px, float* py);
+
+/* compute_shader.wgsl:101-118 set_color. */
+void orc_set_color(float vx, float vy, float max_energy, float rgba[4]);
+/* compute_shader.wgsl:132-142 hash_cell + get_key_from_hash. */
+uint32_t orc_hash_cell(int32_t cx, int32_t cy);
+uint32_t orc_cell_key(int32_t cx, int32_t cy, uint32_t n);
+/* WGSL i32(f32): truncate toward zero, saturate, NaN -> 0. */
+int32_t orc_f32_to_i32(float v);
+
+/* One active stream step (mode STREAM) over n particles with global ids id_offset+i.
+ * life may be NULL when RPS_EXT_LIFETIME is off.  stats may be NULL. */
+void orc_stream_step(const rps_config* cfg, const rps_ext_config* ext, uint64_t id_offset,
+                     uint64_t active_step, float* x, float* y, float* vx, float* vy,
+                     float* life, uint64_t n, orc_stats* stats);
+/* Same, OpenMP-parallel over particles (bench cpu_baseline); identical results. */
+void orc_stream_step_omp(const rps_config* cfg, const rps_ext_config* ext, uint64_t id_offset,
+                         uint64_t active_step, float* x, float* y, float* vx, float* vy,
+                         float* life, uint64_t n, int threads);
+
+/* Device-init restatement (rps_init_scatter). */
+void orc_init_scatter(const rps_config* cfg, const rps_ext_config* ext, uint64_t seed,
+                      uint64_t id_offset, uint64_t global_count, float* x, float* y,
+                      float* vx, float* vy, float* life, uint64_t n);
+
+/* All-pairs softened gravity: acc of targets [t0, t0+nt) from all ns sources. */
+void orc_nbody_accel(const rps_ext_config* ext, const float* sx, const float* sy, uint64_t ns,
+                     uint64_t t0, uint64_t nt, float* ax, float* ay);
+/* Integrate given accelerations (mode NBODY second half). */
+void orc_nbody_integrate(const rps_config* cfg, const rps_ext_config* ext, const float* ax,
+                         const float* ay, float* x, float* y, float* vx, float* vy, uint64_t n);
+
+/* SPH passes (compute_shader.wgsl:455-525, :420-453).  lookup has 2*P uint32 (P =
+ * next_pow2(N)), offsets N, dens 2N, pred 2N. */
+void orc_sph_bin(const rps_config* cfg, const float* x, const float* y, uint32_t* lookup,
+                 uint32_t* offsets, uint32_t n);
+uint32_t orc_sph_sort(uint32_t* lookup, uint32_t n); /* returns number of passes */
+void orc_sph_offsets(const uint32_t* lookup, uint32_t* offsets, uint32_t n);
+void orc_sph_pre(const rps_config* cfg, float* vx, float* vy, const float* x, const float* y,
+                 const uint32_t* lookup, const uint32_t* offsets, float* dens, float* pred,
+                 uint32_t n);
+void orc_sph_sim(const rps_config* cfg, float* x, float* y, float* vx, float* vy,
+                 const uint32_t* lookup, const uint32_t* offsets, const float* dens,
+                 const float* pred, uint32_t n);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

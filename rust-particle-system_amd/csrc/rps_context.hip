@@ -1,0 +1,803 @@
+// rps_context.hip — implementation of the C ABI declared in include/rps.h.
+//
+// Replaces, for the hot path only:
+//   prepare_particle_buffers   (src/particle_buffers.rs:38-237)  -> rps_create / rps_set_config
+//   ParticleComputeNode::run    (src/particle_compute.rs:91-195)  -> rps_step
+//   ParticleComputeNode::update (src/particle_compute.rs:197-199) -> rps_update
+//   read_*_from_gpu             (src/debug.rs:121-265)           -> rps_read_debug
+// Device state is SoA in one hipMalloc arena; every call is ordered on the
+// context's own HIP stream.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "rps_internal.hpp"
+
+using namespace rps;
+
+struct rps_ctx {
+  int device = 0;
+  uint32_t mode = RPS_MODE_STREAM;
+  uint64_t n = 0, id_offset = 0, global_count = 0;
+  hipStream_t stream = nullptr;
+
+  rps_config cfg{};
+  rps_ext_config ext{};
+  bool have_config = false;
+
+  char* arena = nullptr;
+  size_t arena_bytes = 0;
+  float *x = nullptr, *y = nullptr, *vx = nullptr, *vy = nullptr, *life = nullptr;
+  // SPH
+  float *vx2 = nullptr, *vy2 = nullptr;
+  uint2* lookup = nullptr;
+  uint32_t* offsets = nullptr;
+  f2* dens = nullptr;
+  f2* pred = nullptr;
+  uint32_t P = 0;
+  uint32_t sort_passes = 0, sort_launches = 0;
+  // N-body
+  f2* pos_all = nullptr;
+  uint64_t ns_padded = 0;
+  float *ax = nullptr, *ay = nullptr;
+  // device config (pinned upload)
+  rps_config* d_cfg = nullptr;
+  rps_config* h_cfg_pinned = nullptr;
+  hipEvent_t cfg_event = nullptr;
+  // stats
+  StatsPartial* partials = nullptr;
+  uint32_t partial_cap = 0;
+  StatsResult* d_stats = nullptr;
+  bool have_stats = false;
+  // staging for AoS transfers
+  rps_particle* d_staging = nullptr;
+  uint64_t staging_cap = 0;
+  // counters
+  uint64_t active_steps = 0;
+  bool stepped = false;
+  // profiling
+  bool profiling = false;
+  std::vector<hipEvent_t> ev_start, ev_stop;
+  size_t ev_used = 0;
+  // tuning
+  uint32_t stream_grid = 0;  // 0: one-shot grid
+  int nontemporal = 1;
+  // comm
+  ncclComm_t comm = nullptr;
+  int rank = 0, nranks = 1;
+
+  std::string err;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(rps_ctx* ctx, int code, const std::string& msg) {
+  if (ctx)
+    ctx->err = msg;
+  else
+    g_err = msg;
+  return code;
+}
+
+#define RPS_HIP(ctx, call)                                                                   \
+  do {                                                                                       \
+    hipError_t e_ = (call);                                                                  \
+    if (e_ != hipSuccess)                                                                    \
+      return fail((ctx), e_ == hipErrorOutOfMemory ? RPS_ERR_OUT_OF_MEMORY : RPS_ERR_DEVICE, \
+                  std::string(#call) + ": " + hipGetErrorString(e_));                        \
+  } while (0)
+
+size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+uint32_t next_pow2_u32(uint32_t n) {
+  uint32_t p = 1;
+  while (p < n) p <<= 1;
+  return p;
+}
+
+rps_ext_config default_ext() {
+  rps_ext_config e;
+  std::memset(&e, 0, sizeof(e));
+  e.integrator = RPS_INTEGRATOR_EULER;
+  e.shader_delay = 5;  // SHADER_DELAY, compute_shader.wgsl:66
+  e.stats_interval = 1;
+  return e;
+}
+
+// Attractor position at time t; same formula as oracle/rps_oracle.c orc_attractor_pos.
+void attractor_pos(const rps_attractor& a, double t, float& px, float& py) {
+  const double ang = (double)a.angular_velocity * t + (double)a.phase;
+  px = (float)((double)a.center[0] + (double)a.orbit_radius * std::cos(ang));
+  py = (float)((double)a.center[1] + (double)a.orbit_radius * std::sin(ang));
+}
+
+int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return v && *v ? std::atoi(v) : dflt;
+}
+
+int check_ctx(rps_ctx* ctx) {
+  if (!ctx) return fail(nullptr, RPS_ERR_INVALID_ARGUMENT, "null context");
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return fail(ctx, RPS_ERR_DEVICE, std::string("hipSetDevice: ") + hipGetErrorString(e));
+  return RPS_OK;
+}
+
+float* field_ptr(rps_ctx* ctx, int field) {
+  switch (field) {
+    case RPS_FIELD_X: return ctx->x;
+    case RPS_FIELD_Y: return ctx->y;
+    case RPS_FIELD_VX: return ctx->vx;
+    case RPS_FIELD_VY: return ctx->vy;
+    case RPS_FIELD_LIFE: return ctx->life;
+    default: return nullptr;
+  }
+}
+
+int ensure_staging(rps_ctx* ctx, uint64_t want) {
+  if (ctx->staging_cap >= want) return RPS_OK;
+  if (ctx->d_staging) RPS_HIP(ctx, hipFree(ctx->d_staging));
+  ctx->d_staging = nullptr;
+  ctx->staging_cap = 0;
+  RPS_HIP(ctx, hipMalloc(&ctx->d_staging, want * sizeof(rps_particle)));
+  ctx->staging_cap = want;
+  return RPS_OK;
+}
+
+constexpr uint64_t kStagingChunk = 1ull << 21;  // 2 Mi particles = 64 MiB of AoS per chunk
+
+StreamArgs make_stream_args(const rps_ctx* ctx, uint64_t k) {
+  StreamArgs a;
+  std::memset(&a, 0, sizeof(a));
+  const rps_config& c = ctx->cfg;
+  const rps_ext_config& e = ctx->ext;
+  a.x = ctx->x;
+  a.y = ctx->y;
+  a.vx = ctx->vx;
+  a.vy = ctx->vy;
+  a.life = ctx->life;
+  a.partials = ctx->partials;
+  a.n = ctx->n;
+  a.id_offset = ctx->id_offset;
+  const float dt = c.fixed_delta_time;
+  a.dt = dt;
+  a.gx_dt = 0.0f * dt;  // vec2(0.0, -gravity) * dt, compute_shader.wgsl:399
+  a.gy_dt = (-c.gravity) * dt;
+  a.neg_g = -c.gravity;
+  a.half_dt = 0.5f * dt;
+  a.half_dt2 = (0.5f * dt) * dt;
+  a.drag_on = e.drag != 0.0f;
+  a.drag_f = 1.0f - e.drag * dt;
+  a.na = std::min<uint32_t>(e.num_attractors, RPS_MAX_ATTRACTORS);
+  const double t = (double)k * (double)dt;
+  for (uint32_t i = 0; i < a.na; ++i) {
+    attractor_pos(e.attractors[i], t, a.ax[i], a.ay[i]);
+    a.as[i] = e.attractors[i].strength;
+    a.ae2[i] = e.attractors[i].softening * e.attractors[i].softening;
+  }
+  a.x_min = c.screen_bounds[0];
+  a.x_max = c.screen_bounds[1];
+  a.y_min = c.screen_bounds[2];
+  a.y_max = c.screen_bounds[3];
+  a.damping = c.damping_factor;
+  a.emit_cx = e.emitter_center[0];
+  a.emit_cy = e.emitter_center[1];
+  a.emit_r = e.emitter_radius;
+  a.spd_min = e.spawn_speed_min;
+  a.spd_range = e.spawn_speed_max - e.spawn_speed_min;
+  a.life_min = e.life_min;
+  a.life_range = e.life_max - e.life_min;
+  a.key0 = (uint32_t)e.seed;
+  a.key1 = (uint32_t)(e.seed >> 32);
+  a.step_lo = (uint32_t)k;
+  a.step_hi = (uint32_t)(k >> 32);
+  return a;
+}
+
+int prof_begin(rps_ctx* ctx) {
+  if (!ctx->profiling) return RPS_OK;
+  if (ctx->ev_used == ctx->ev_start.size()) {
+    hipEvent_t a, b;
+    RPS_HIP(ctx, hipEventCreate(&a));
+    RPS_HIP(ctx, hipEventCreate(&b));
+    ctx->ev_start.push_back(a);
+    ctx->ev_stop.push_back(b);
+  }
+  RPS_HIP(ctx, hipEventRecord(ctx->ev_start[ctx->ev_used], ctx->stream));
+  return RPS_OK;
+}
+
+int prof_end(rps_ctx* ctx) {
+  if (!ctx->profiling) return RPS_OK;
+  RPS_HIP(ctx, hipEventRecord(ctx->ev_stop[ctx->ev_used], ctx->stream));
+  ++ctx->ev_used;
+  return RPS_OK;
+}
+
+SphBuffers sph_buffers(rps_ctx* ctx) {
+  SphBuffers b;
+  b.cfg = ctx->d_cfg;
+  b.x = ctx->x;
+  b.y = ctx->y;
+  b.vx = ctx->vx;
+  b.vy = ctx->vy;
+  b.vx2 = ctx->vx2;
+  b.vy2 = ctx->vy2;
+  b.lookup = ctx->lookup;
+  b.offsets = ctx->offsets;
+  b.dens = ctx->dens;
+  b.pred = ctx->pred;
+  b.n = (uint32_t)ctx->n;
+  b.p = ctx->P;
+  return b;
+}
+
+int step_stream(rps_ctx* ctx) {
+  const uint64_t k = ctx->active_steps;
+  const rps_ext_config& e = ctx->ext;
+  const bool stats = (e.flags & RPS_EXT_STATS) && (k % std::max<uint32_t>(e.stats_interval, 1u) == 0);
+  StreamArgs a = make_stream_args(ctx, k);
+  StreamLaunch l;
+  l.verlet = e.integrator == RPS_INTEGRATOR_VERLET;
+  l.lifetime = (e.flags & RPS_EXT_LIFETIME) != 0;
+  l.stats = stats;
+  l.nontemporal = ctx->nontemporal;
+  const uint32_t oneshot = stream_blocks_for(ctx->n);
+  l.grid = ctx->stream_grid ? std::min(ctx->stream_grid, oneshot) : oneshot;
+  if (stats && l.grid > ctx->partial_cap) {
+    if (ctx->partials) RPS_HIP(ctx, hipFree(ctx->partials));
+    ctx->partials = nullptr;
+    RPS_HIP(ctx, hipMalloc(&ctx->partials, sizeof(StatsPartial) * l.grid));
+    ctx->partial_cap = l.grid;
+    a.partials = ctx->partials;
+  }
+  int rc = prof_begin(ctx);
+  if (rc) return rc;
+  RPS_HIP(ctx, launch_stream_step(a, l, ctx->stream));
+  rc = prof_end(ctx);
+  if (rc) return rc;
+  if (stats) {
+    RPS_HIP(ctx, launch_stats_finalize(ctx->partials, l.grid, ctx->d_stats, k, ctx->stream));
+    ctx->have_stats = true;
+  }
+  return RPS_OK;
+}
+
+int step_nbody(rps_ctx* ctx) {
+  const rps_config& c = ctx->cfg;
+  const rps_ext_config& e = ctx->ext;
+  RPS_HIP(ctx, launch_nbody_pack(ctx->x, ctx->y, ctx->pos_all + ctx->id_offset, ctx->n, ctx->stream));
+  if (ctx->nranks > 1) {
+    // In-place all-gather of every rank's float2 positions over xGMI.
+    ncclResult_t r = ncclAllGather(ctx->pos_all + ctx->id_offset, ctx->pos_all, ctx->n * 2,
+                                   ncclFloat, ctx->comm, ctx->stream);
+    if (r != ncclSuccess)
+      return fail(ctx, RPS_ERR_COMM, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+  }
+  const float eps2 = e.nbody_softening * e.nbody_softening;
+  int rc = prof_begin(ctx);
+  if (rc) return rc;
+  RPS_HIP(ctx, launch_nbody_accel(ctx->pos_all, ctx->ns_padded, ctx->id_offset, ctx->n, eps2,
+                                  e.nbody_strength, ctx->ax, ctx->ay, ctx->stream));
+  rc = prof_end(ctx);
+  if (rc) return rc;
+  NbodyIntegrateArgs ia;
+  ia.x = ctx->x;
+  ia.y = ctx->y;
+  ia.vx = ctx->vx;
+  ia.vy = ctx->vy;
+  ia.ax = ctx->ax;
+  ia.ay = ctx->ay;
+  ia.n = ctx->n;
+  ia.dt = c.fixed_delta_time;
+  ia.gx_dt = 0.0f * c.fixed_delta_time;
+  ia.gy_dt = (-c.gravity) * c.fixed_delta_time;
+  ia.drag_on = e.drag != 0.0f;
+  ia.drag_f = 1.0f - e.drag * c.fixed_delta_time;
+  ia.x_min = c.screen_bounds[0];
+  ia.x_max = c.screen_bounds[1];
+  ia.y_min = c.screen_bounds[2];
+  ia.y_max = c.screen_bounds[3];
+  ia.damping = c.damping_factor;
+  RPS_HIP(ctx, launch_nbody_integrate(ia, ctx->stream));
+  return RPS_OK;
+}
+
+int step_sph_grid(rps_ctx* ctx) {
+  SphBuffers b = sph_buffers(ctx);
+  RPS_HIP(ctx, launch_sph_bin(b, ctx->stream));
+  RPS_HIP(ctx, launch_sph_sort(b, ctx->stream, &ctx->sort_passes, &ctx->sort_launches));
+  RPS_HIP(ctx, launch_sph_offsets(b, ctx->stream));
+  return RPS_OK;
+}
+
+int step_sph_sim(rps_ctx* ctx) {
+  SphBuffers b = sph_buffers(ctx);
+  RPS_HIP(ctx, launch_sph_pre(b, ctx->stream));
+  int rc = prof_begin(ctx);
+  if (rc) return rc;
+  RPS_HIP(ctx, launch_sph_sim(b, ctx->stream));
+  rc = prof_end(ctx);
+  if (rc) return rc;
+  std::swap(ctx->vx, ctx->vx2);
+  std::swap(ctx->vy, ctx->vy2);
+  return RPS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t rps_abi_version(void) { return RPS_ABI_VERSION; }
+
+const char* rps_status_string(int status) {
+  switch (status) {
+    case RPS_OK: return "ok";
+    case RPS_ERR_INVALID_ARGUMENT: return "invalid argument";
+    case RPS_ERR_DEVICE: return "device error";
+    case RPS_ERR_OUT_OF_MEMORY: return "out of memory";
+    case RPS_ERR_UNSUPPORTED: return "unsupported";
+    case RPS_ERR_COMM: return "communication error";
+    case RPS_ERR_NO_DEVICE: return "no device";
+    default: return "unknown status";
+  }
+}
+
+int rps_device_count(int* count) {
+  if (!count) return fail(nullptr, RPS_ERR_INVALID_ARGUMENT, "null count");
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) {
+    *count = 0;
+    return fail(nullptr, RPS_ERR_NO_DEVICE, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+  }
+  *count = c;
+  return RPS_OK;
+}
+
+const char* rps_last_error(const rps_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
+
+int rps_create(const rps_create_info* info, rps_ctx** out) {
+  if (!info || !out) return fail(nullptr, RPS_ERR_INVALID_ARGUMENT, "null argument");
+  *out = nullptr;
+  if (info->mode > RPS_MODE_SPH) return fail(nullptr, RPS_ERR_INVALID_ARGUMENT, "bad mode");
+  // NonZeroU64::new(particle_buffer_size).unwrap() (src/particle_buffers.rs:73-74)
+  if (info->particle_count == 0) return fail(nullptr, RPS_ERR_INVALID_ARGUMENT, "particle_count must be > 0");
+  const uint64_t global = info->global_count ? info->global_count : info->id_offset + info->particle_count;
+  if (info->id_offset + info->particle_count > global)
+    return fail(nullptr, RPS_ERR_INVALID_ARGUMENT, "id_offset + particle_count > global_count");
+  if (info->mode == RPS_MODE_SPH) {
+    if (info->particle_count > 0x80000000ull || info->id_offset != 0 || global != info->particle_count)
+      return fail(nullptr, RPS_ERR_INVALID_ARGUMENT,
+                  "SPH mode: one unsharded system of at most 2^31 particles (u32 keys, wgsl:52)");
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return fail(nullptr, RPS_ERR_NO_DEVICE, "no HIP device visible");
+  if (info->device < 0 || info->device >= ndev)
+    return fail(nullptr, RPS_ERR_INVALID_ARGUMENT, "device ordinal out of range");
+
+  rps_ctx* ctx = new (std::nothrow) rps_ctx();
+  if (!ctx) return fail(nullptr, RPS_ERR_OUT_OF_MEMORY, "host allocation failed");
+  ctx->device = info->device;
+  ctx->mode = info->mode;
+  ctx->n = info->particle_count;
+  ctx->id_offset = info->id_offset;
+  ctx->global_count = global;
+  ctx->ext = default_ext();
+  ctx->stream_grid = (uint32_t)std::max(0, env_int("RPS_STREAM_GRID", 0));
+  ctx->nontemporal = env_int("RPS_STREAM_NT", 1) != 0;
+
+  auto bail = [&](int code) {
+    std::string m = ctx->err;
+    rps_destroy(ctx);
+    g_err = m;
+    return code;
+  };
+  if (hipSetDevice(ctx->device) != hipSuccess) {
+    ctx->err = "hipSetDevice failed";
+    return bail(RPS_ERR_DEVICE);
+  }
+  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    ctx->err = "hipStreamCreate failed";
+    return bail(RPS_ERR_DEVICE);
+  }
+
+  // Carve the arena: every array 256-B aligned (16-B vector access + full cache lines).
+  const size_t n = ctx->n;
+  const size_t nf = align_up(n * sizeof(float), 256);
+  size_t off = 0;
+  struct Slot { void** p; size_t bytes; };
+  std::vector<Slot> slots;
+  slots.push_back({(void**)&ctx->x, nf});
+  slots.push_back({(void**)&ctx->y, nf});
+  slots.push_back({(void**)&ctx->vx, nf});
+  slots.push_back({(void**)&ctx->vy, nf});
+  if (ctx->mode == RPS_MODE_STREAM) slots.push_back({(void**)&ctx->life, nf});
+  if (ctx->mode == RPS_MODE_SPH) {
+    ctx->P = next_pow2_u32((uint32_t)n);  // spatial lookup sized next_pow2 (particle_buffers.rs:86)
+    slots.push_back({(void**)&ctx->vx2, nf});
+    slots.push_back({(void**)&ctx->vy2, nf});
+    slots.push_back({(void**)&ctx->lookup, align_up((size_t)ctx->P * sizeof(uint2), 256)});
+    slots.push_back({(void**)&ctx->offsets, align_up(n * sizeof(uint32_t), 256)});
+    slots.push_back({(void**)&ctx->dens, align_up(n * sizeof(f2), 256)});
+    slots.push_back({(void**)&ctx->pred, align_up(n * sizeof(f2), 256)});
+  }
+  if (ctx->mode == RPS_MODE_NBODY) {
+    ctx->ns_padded = (global + kNbodyTile - 1) / kNbodyTile * kNbodyTile;
+    slots.push_back({(void**)&ctx->pos_all, align_up(ctx->ns_padded * sizeof(f2), 256)});
+    slots.push_back({(void**)&ctx->ax, nf});
+    slots.push_back({(void**)&ctx->ay, nf});
+  }
+  slots.push_back({(void**)&ctx->d_cfg, align_up(sizeof(rps_config), 256)});
+  slots.push_back({(void**)&ctx->d_stats, align_up(sizeof(StatsResult), 256)});
+  std::vector<size_t> offs;
+  for (auto& s : slots) {
+    offs.push_back(off);
+    off += s.bytes;
+  }
+  ctx->arena_bytes = off;
+  hipError_t e = hipMalloc(&ctx->arena, ctx->arena_bytes);
+  if (e != hipSuccess) {
+    ctx->err = std::string("hipMalloc(") + std::to_string(ctx->arena_bytes) + "): " + hipGetErrorString(e);
+    return bail(e == hipErrorOutOfMemory ? RPS_ERR_OUT_OF_MEMORY : RPS_ERR_DEVICE);
+  }
+  for (size_t i = 0; i < slots.size(); ++i) *slots[i].p = ctx->arena + offs[i];
+  // wgpu buffers are zero-initialised; the SPH lookup pad entries rely on it.
+  if (hipMemsetAsync(ctx->arena, 0, ctx->arena_bytes, ctx->stream) != hipSuccess) {
+    ctx->err = "hipMemsetAsync failed";
+    return bail(RPS_ERR_DEVICE);
+  }
+  if (ctx->mode == RPS_MODE_NBODY &&
+      launch_nbody_pad(ctx->pos_all, global, ctx->ns_padded, ctx->stream) != hipSuccess) {
+    ctx->err = "nbody pad launch failed";
+    return bail(RPS_ERR_DEVICE);
+  }
+  if (hipHostMalloc((void**)&ctx->h_cfg_pinned, sizeof(rps_config), hipHostMallocDefault) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->cfg_event, hipEventDisableTiming) != hipSuccess) {
+    ctx->err = "pinned config staging failed";
+    return bail(RPS_ERR_OUT_OF_MEMORY);
+  }
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess) {
+    ctx->err = "hipStreamSynchronize failed";
+    return bail(RPS_ERR_DEVICE);
+  }
+  *out = ctx;
+  return RPS_OK;
+}
+
+int rps_destroy(rps_ctx* ctx) {
+  if (!ctx) return RPS_OK;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->comm) ncclCommDestroy(ctx->comm);
+  for (auto ev : ctx->ev_start) (void)hipEventDestroy(ev);
+  for (auto ev : ctx->ev_stop) (void)hipEventDestroy(ev);
+  if (ctx->cfg_event) (void)hipEventDestroy(ctx->cfg_event);
+  if (ctx->h_cfg_pinned) (void)hipHostFree(ctx->h_cfg_pinned);
+  if (ctx->d_staging) (void)hipFree(ctx->d_staging);
+  if (ctx->partials) (void)hipFree(ctx->partials);
+  if (ctx->arena) (void)hipFree(ctx->arena);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return RPS_OK;
+}
+
+int rps_set_config(rps_ctx* ctx, const rps_config* cfg, const rps_ext_config* ext) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!cfg) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "null config");
+  rps_ext_config e = ext ? *ext : default_ext();
+  if (e.integrator > RPS_INTEGRATOR_VERLET) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "bad integrator");
+  if (e.num_attractors > RPS_MAX_ATTRACTORS)
+    return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "num_attractors > RPS_MAX_ATTRACTORS");
+  if (ctx->mode != RPS_MODE_STREAM && (e.flags & (RPS_EXT_LIFETIME | RPS_EXT_STATS)))
+    return fail(ctx, RPS_ERR_UNSUPPORTED, "lifetime/stats extensions exist in STREAM mode only");
+  if (ctx->mode != RPS_MODE_STREAM && (e.integrator != RPS_INTEGRATOR_EULER || e.num_attractors))
+    return fail(ctx, RPS_ERR_UNSUPPORTED, "attractors/Verlet exist in STREAM mode only");
+  if (ctx->mode == RPS_MODE_NBODY && !(e.nbody_softening > 0.0f))
+    return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "nbody_softening must be > 0");
+  if (ctx->mode == RPS_MODE_SPH && cfg->particle_count != (uint32_t)ctx->n)
+    return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "SPH mode: config.particle_count must equal the context's particles");
+  if (!(cfg->fixed_delta_time == cfg->fixed_delta_time))
+    return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "fixed_delta_time is NaN");
+  ctx->cfg = *cfg;
+  ctx->ext = e;
+  ctx->have_config = true;
+  // write_buffer(config) (src/particle_buffers.rs:230-236): pinned staging -> device.  The
+  // staging slot is reused only after the previous copy has drained.
+  RPS_HIP(ctx, hipEventSynchronize(ctx->cfg_event));
+  std::memcpy(ctx->h_cfg_pinned, cfg, sizeof(rps_config));
+  RPS_HIP(ctx, hipMemcpyAsync(ctx->d_cfg, ctx->h_cfg_pinned, sizeof(rps_config),
+                              hipMemcpyHostToDevice, ctx->stream));
+  RPS_HIP(ctx, hipEventRecord(ctx->cfg_event, ctx->stream));
+  return RPS_OK;
+}
+
+int rps_get_config(const rps_ctx* ctx, rps_config* cfg, rps_ext_config* ext) {
+  if (!ctx) return fail(nullptr, RPS_ERR_INVALID_ARGUMENT, "null context");
+  if (cfg) *cfg = ctx->cfg;
+  if (ext) *ext = ctx->ext;
+  return RPS_OK;
+}
+
+int rps_upload_particles(rps_ctx* ctx, const rps_particle* aos, uint64_t offset, uint64_t n) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!aos && n) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "null particles");
+  if (offset + n > ctx->n) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "range exceeds particle_count");
+  const uint64_t chunk = std::min<uint64_t>(n, kStagingChunk);
+  if (n == 0) return RPS_OK;
+  rc = ensure_staging(ctx, chunk);
+  if (rc) return rc;
+  for (uint64_t done = 0; done < n; done += chunk) {
+    const uint64_t m = std::min(chunk, n - done);
+    RPS_HIP(ctx, hipMemcpyAsync(ctx->d_staging, aos + done, m * sizeof(rps_particle),
+                                hipMemcpyHostToDevice, ctx->stream));
+    const uint64_t o = offset + done;
+    RPS_HIP(ctx, launch_aos_to_soa(ctx->d_staging, ctx->x + o, ctx->y + o, ctx->vx + o,
+                                   ctx->vy + o, m, ctx->stream));
+    RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  }
+  return RPS_OK;
+}
+
+int rps_download_particles(rps_ctx* ctx, rps_particle* aos, uint64_t offset, uint64_t n) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!aos && n) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "null particles");
+  if (offset + n > ctx->n) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "range exceeds particle_count");
+  if (n == 0) return RPS_OK;
+  const uint64_t chunk = std::min<uint64_t>(n, kStagingChunk);
+  rc = ensure_staging(ctx, chunk);
+  if (rc) return rc;
+  for (uint64_t done = 0; done < n; done += chunk) {
+    const uint64_t m = std::min(chunk, n - done);
+    const uint64_t o = offset + done;
+    RPS_HIP(ctx, launch_soa_to_aos(ctx->x + o, ctx->y + o, ctx->vx + o, ctx->vy + o, ctx->d_staging,
+                                   m, ctx->cfg.max_energy, ctx->stepped ? 0 : 1, ctx->stream));
+    RPS_HIP(ctx, hipMemcpyAsync(aos + done, ctx->d_staging, m * sizeof(rps_particle),
+                                hipMemcpyDeviceToHost, ctx->stream));
+    RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  }
+  return RPS_OK;
+}
+
+int rps_upload_field(rps_ctx* ctx, int field, const float* src, uint64_t offset, uint64_t n) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  float* p = field_ptr(ctx, field);
+  if (!p) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "field not present in this mode");
+  if (!src && n) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "null source");
+  if (offset + n > ctx->n) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "range exceeds particle_count");
+  if (n == 0) return RPS_OK;
+  RPS_HIP(ctx, hipMemcpyAsync(p + offset, src, n * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+  RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return RPS_OK;
+}
+
+int rps_download_field(rps_ctx* ctx, int field, float* dst, uint64_t offset, uint64_t n) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  float* p = field_ptr(ctx, field);
+  if (!p) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "field not present in this mode");
+  if (!dst && n) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "null destination");
+  if (offset + n > ctx->n) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "range exceeds particle_count");
+  if (n == 0) return RPS_OK;
+  RPS_HIP(ctx, hipMemcpyAsync(dst, p + offset, n * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+  RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return RPS_OK;
+}
+
+int rps_read_debug(rps_ctx* ctx, int which, void* dst, uint64_t bytes) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!dst) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "null destination");
+  const void* src = nullptr;
+  uint64_t want = 0;
+  switch (which) {
+    case RPS_DEBUG_SPATIAL_LOOKUP: src = ctx->lookup; want = (uint64_t)ctx->P * 8; break;
+    case RPS_DEBUG_LOOKUP_OFFSETS: src = ctx->offsets; want = ctx->n * 4; break;
+    case RPS_DEBUG_DENSITIES: src = ctx->dens; want = ctx->n * 8; break;
+    case RPS_DEBUG_PREDICTED: src = ctx->pred; want = ctx->n * 8; break;
+    case RPS_DEBUG_ACCEL_X: src = ctx->ax; want = ctx->n * 4; break;
+    case RPS_DEBUG_ACCEL_Y: src = ctx->ay; want = ctx->n * 4; break;
+    default: return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "unknown debug buffer");
+  }
+  if (!src) return fail(ctx, RPS_ERR_UNSUPPORTED, "debug buffer not present in this mode");
+  if (bytes != want)
+    return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "bytes must equal the buffer size (" + std::to_string(want) + ")");
+  RPS_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return RPS_OK;
+}
+
+int rps_init_scatter(rps_ctx* ctx, uint64_t seed) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!ctx->have_config) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "rps_set_config first");
+  InitArgs a;
+  a.x = ctx->x;
+  a.y = ctx->y;
+  a.vx = ctx->vx;
+  a.vy = ctx->vy;
+  a.life = (ctx->mode == RPS_MODE_STREAM) ? ctx->life : nullptr;
+  a.n = ctx->n;
+  a.id_offset = ctx->id_offset;
+  a.x_min = ctx->cfg.screen_bounds[0];
+  a.x_max = ctx->cfg.screen_bounds[1];
+  a.y_min = ctx->cfg.screen_bounds[2];
+  a.y_max = ctx->cfg.screen_bounds[3];
+  a.global_count_f = (float)ctx->global_count;
+  a.life_min = ctx->ext.life_min;
+  a.life_range = ctx->ext.life_max - ctx->ext.life_min;
+  a.key0 = (uint32_t)seed;
+  a.key1 = (uint32_t)(seed >> 32);
+  RPS_HIP(ctx, launch_init_scatter(a, ctx->stream));
+  return RPS_OK;
+}
+
+int rps_step(rps_ctx* ctx, uint32_t nsteps) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!ctx->have_config) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "rps_set_config first");
+  if (ctx->mode == RPS_MODE_NBODY && ctx->nranks > 1 && !ctx->comm)
+    return fail(ctx, RPS_ERR_COMM, "sharded N-body needs rps_comm_init");
+  if (ctx->mode == RPS_MODE_NBODY && ctx->global_count != ctx->n && !ctx->comm)
+    return fail(ctx, RPS_ERR_COMM, "sharded N-body needs rps_comm_init");
+  for (uint32_t s = 0; s < nsteps; ++s) {
+    ctx->cfg.frame_count += 1;  // src/particle_buffers.rs:227
+    const bool active = ctx->cfg.frame_count >= ctx->ext.shader_delay;  // wgsl:426, :442
+    if (ctx->mode == RPS_MODE_SPH) {
+      rc = step_sph_grid(ctx);  // passes 1-3 run every frame (particle_compute.rs:105-163)
+      if (rc) return rc;
+    }
+    if (!active) continue;
+    switch (ctx->mode) {
+      case RPS_MODE_STREAM: rc = step_stream(ctx); break;
+      case RPS_MODE_NBODY: rc = step_nbody(ctx); break;
+      default: rc = step_sph_sim(ctx); break;
+    }
+    if (rc) return rc;
+    ++ctx->active_steps;
+    ctx->stepped = true;
+  }
+  return RPS_OK;
+}
+
+int rps_update(rps_ctx* ctx) { return ctx ? RPS_OK : fail(nullptr, RPS_ERR_INVALID_ARGUMENT, "null context"); }
+
+int rps_sync(rps_ctx* ctx) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return RPS_OK;
+}
+
+int rps_get_stats(rps_ctx* ctx, rps_stats* out) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!out) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "null output");
+  if (!ctx->have_stats) return fail(ctx, RPS_ERR_UNSUPPORTED, "no stats reduced yet (RPS_EXT_STATS)");
+  StatsResult r;
+  RPS_HIP(ctx, hipMemcpyAsync(&r, ctx->d_stats, sizeof(r), hipMemcpyDeviceToHost, ctx->stream));
+  RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  for (int k = 0; k < 4; ++k) out->bbox[k] = r.bbox[k];
+  out->kinetic_energy = r.ke;
+  out->particles = r.count;
+  out->respawned = r.respawned;
+  out->step = r.step;
+  return RPS_OK;
+}
+
+int rps_get_counters(const rps_ctx* ctx, uint32_t* frame_count, uint64_t* active_steps) {
+  if (!ctx) return fail(nullptr, RPS_ERR_INVALID_ARGUMENT, "null context");
+  if (frame_count) *frame_count = ctx->cfg.frame_count;
+  if (active_steps) *active_steps = ctx->active_steps;
+  return RPS_OK;
+}
+
+int rps_set_profiling(rps_ctx* ctx, int enable) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  ctx->profiling = enable != 0;
+  ctx->ev_used = 0;
+  return RPS_OK;
+}
+
+int rps_get_kernel_time(rps_ctx* ctx, double* avg_ms, uint64_t* launches) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  double total = 0.0;
+  for (size_t i = 0; i < ctx->ev_used; ++i) {
+    float ms = 0.0f;
+    RPS_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev_start[i], ctx->ev_stop[i]));
+    total += ms;
+  }
+  if (avg_ms) *avg_ms = ctx->ev_used ? total / (double)ctx->ev_used : 0.0;
+  if (launches) *launches = ctx->ev_used;
+  ctx->ev_used = 0;
+  return RPS_OK;
+}
+
+int rps_time_steps(rps_ctx* ctx, uint32_t nsteps, double* total_ms) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  hipEvent_t a, b;
+  RPS_HIP(ctx, hipEventCreate(&a));
+  RPS_HIP(ctx, hipEventCreate(&b));
+  RPS_HIP(ctx, hipEventRecord(a, ctx->stream));
+  rc = rps_step(ctx, nsteps);
+  if (rc == RPS_OK) {
+    RPS_HIP(ctx, hipEventRecord(b, ctx->stream));
+    RPS_HIP(ctx, hipEventSynchronize(b));
+    float ms = 0.0f;
+    RPS_HIP(ctx, hipEventElapsedTime(&ms, a, b));
+    if (total_ms) *total_ms = ms;
+  }
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  return rc;
+}
+
+void* rps_get_stream(rps_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int rps_step_cost(const rps_ctx* ctx, double* amount, int* unit) {
+  if (!ctx || !amount || !unit) return fail(nullptr, RPS_ERR_INVALID_ARGUMENT, "null argument");
+  switch (ctx->mode) {
+    case RPS_MODE_STREAM: {
+      // r+w of x, y, vx, vy (+ life): DESIGN.md §5.
+      const double per = (ctx->ext.flags & RPS_EXT_LIFETIME) ? 40.0 : 32.0;
+      *amount = per * (double)ctx->n;
+      *unit = 0;
+      return RPS_OK;
+    }
+    case RPS_MODE_NBODY:
+      *amount = 20.0 * (double)ctx->n * (double)ctx->global_count;  // GPU Gems 3 ch.31 convention
+      *unit = 1;
+      return RPS_OK;
+    default:
+      return fail(const_cast<rps_ctx*>(ctx), RPS_ERR_UNSUPPORTED, "no closed-form cost for SPH mode");
+  }
+}
+
+int rps_comm_unique_id(void* out128) {
+  if (!out128) return fail(nullptr, RPS_ERR_INVALID_ARGUMENT, "null output");
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId must be 128 bytes");
+  ncclUniqueId id;
+  ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) return fail(nullptr, RPS_ERR_COMM, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+  std::memcpy(out128, &id, sizeof(id));
+  return RPS_OK;
+}
+
+int rps_comm_init(rps_ctx* ctx, int rank, int nranks, const void* unique_id128) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!unique_id128 || nranks < 1 || rank < 0 || rank >= nranks)
+    return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "bad rank/nranks/unique id");
+  if (ctx->mode == RPS_MODE_NBODY &&
+      (ctx->global_count != ctx->n * (uint64_t)nranks || ctx->id_offset != ctx->n * (uint64_t)rank))
+    return fail(ctx, RPS_ERR_INVALID_ARGUMENT,
+                "sharded N-body needs equal contiguous shards: global = nranks*n, id_offset = rank*n");
+  ncclUniqueId id;
+  std::memcpy(&id, unique_id128, sizeof(id));
+  ncclResult_t r = ncclCommInitRank(&ctx->comm, nranks, id, rank);
+  if (r != ncclSuccess) return fail(ctx, RPS_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  ctx->rank = rank;
+  ctx->nranks = nranks;
+  return RPS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,255 @@
+// rps_device.hpp — per-particle device math for gfx950.
+//
+// Every function here computes, operation for operation, what assets/compute_shader.wgsl
+// (or the build-defined extension spec in DESIGN.md §3.2) prescribes.  The whole library is
+// compiled with -ffp-contract=off and without fast-math, so each a*b+c is two IEEE
+// roundings and division/sqrt are correctly rounded: results are bit-identical to the CPU
+// restatement in oracle/ (which is only a test-side checker; nothing here links it).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rps {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+constexpr int kMaxAttractors = 8;
+
+// Per-step uniforms of the streaming kernel.  Passed by value: the kernarg segment lands in
+// SGPRs through s_load, so the 4-8 attractors cost no LDS and no VGPRs.
+struct StreamArgs {
+  float* __restrict__ x;
+  float* __restrict__ y;
+  float* __restrict__ vx;
+  float* __restrict__ vy;
+  float* __restrict__ life;
+  struct StatsPartial* partials;  // one per workgroup when stats are on
+  uint64_t n;                     // particles in this shard
+  uint64_t id_offset;             // global id of particle 0
+  float dt, gx_dt, gy_dt, neg_g, half_dt, half_dt2, drag_f;
+  uint32_t drag_on;
+  uint32_t na;
+  float ax[kMaxAttractors], ay[kMaxAttractors], as[kMaxAttractors], ae2[kMaxAttractors];
+  float x_min, x_max, y_min, y_max, damping;
+  float emit_cx, emit_cy, emit_r, spd_min, spd_range, life_min, life_range;
+  uint32_t key0, key1, step_lo, step_hi;
+};
+
+struct StatsPartial {  // 48 B, written once per workgroup, reduced in fixed order
+  float bbox[4];
+  double ke;
+  unsigned long long count;
+  unsigned long long respawned;
+  unsigned long long _pad;
+};
+
+struct StatsResult {
+  float bbox[4];
+  double ke;
+  unsigned long long count;
+  unsigned long long respawned;
+  unsigned long long step;
+};
+
+// ---------------------------------------------------------------------------------------
+// Random123 Philox4x32-10 (build-defined respawn stream, keyed by (seed, global id, step)).
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                              uint32_t k0, uint32_t k1, uint32_t out[4]) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r > 0) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    const uint32_t lo0 = 0xD2511F53u * c0;
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c0);
+    const uint32_t lo1 = 0xCD9E8D57u * c2;
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2);
+    const uint32_t n0 = hi1 ^ c1 ^ k0;
+    const uint32_t n2 = hi0 ^ c3 ^ k1;
+    c0 = n0;
+    c1 = lo1;
+    c2 = n2;
+    c3 = lo0;
+  }
+  out[0] = c0;
+  out[1] = c1;
+  out[2] = c2;
+  out[3] = c3;
+}
+
+__device__ __forceinline__ float u01(uint32_t w) {
+  return (float)(w >> 8) * (1.0f / 16777216.0f);
+}
+
+// sin/cos(2*pi*u): quadrant split + fixed-order Taylor polynomials.
+__device__ __forceinline__ void sincos_turns(float u, float& c_out, float& s_out) {
+  const float u4 = u * 4.0f;
+  const int q = (int)u4;
+  const float f = u4 - (float)q;
+  const float th = f * 1.57079632679489662f;
+  const float t2 = th * th;
+  float sp = -2.50521083854417188e-08f;
+  sp = sp * t2 + 2.75573192239858907e-06f;
+  sp = sp * t2 + -1.98412698412698413e-04f;
+  sp = sp * t2 + 8.33333333333333333e-03f;
+  sp = sp * t2 + -1.66666666666666667e-01f;
+  const float s = th + (th * t2) * sp;
+  float cp = 2.08767569878680990e-09f;
+  cp = cp * t2 + -2.75573192239858907e-07f;
+  cp = cp * t2 + 2.48015873015873016e-05f;
+  cp = cp * t2 + -1.38888888888888889e-03f;
+  cp = cp * t2 + 4.16666666666666667e-02f;
+  cp = cp * t2 + -0.5f;
+  const float c = 1.0f + t2 * cp;
+  switch (q & 3) {
+    case 0: c_out = c; s_out = s; break;
+    case 1: c_out = -s; s_out = c; break;
+    case 2: c_out = -c; s_out = -s; break;
+    default: c_out = s; s_out = -c; break;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Reference helpers
+// ---------------------------------------------------------------------------------------
+
+// check_screen_bounds, compute_shader.wgsl:69-99.
+__device__ __forceinline__ void wall(float x_min, float x_max, float y_min, float y_max,
+                                     float damp, float& x, float& y, float& vx, float& vy) {
+  if (x <= x_min) {
+    x = x_min;
+    vx = fabsf(vx) * damp;
+  } else if (x >= x_max) {
+    x = x_max;
+    vx = -fabsf(vx) * damp;
+  }
+  if (y <= y_min) {
+    y = y_min;
+    vy = fabsf(vy) * damp;
+  } else if (y >= y_max) {
+    y = y_max;
+    vy = -fabsf(vy) * damp;
+  }
+}
+
+// set_color, compute_shader.wgsl:101-118.
+__device__ __forceinline__ f4 set_color(float vx, float vy, float max_energy) {
+  const float speed_sq = vx * vx + vy * vy;
+  const float energy = 0.5f * speed_sq;
+  float nrm = energy / max_energy;
+  nrm = nrm < 0.0f ? 0.0f : nrm;
+  nrm = nrm > 1.0f ? 1.0f : nrm;
+  f4 rgba;
+  if (nrm < 0.5f) {
+    const float t = nrm * 2.0f;
+    rgba = f4{0.0f, t, 1.0f - t, 1.0f};
+  } else {
+    const float t = (nrm - 0.5f) * 2.0f;
+    rgba = f4{t, 1.0f - t, 0.0f, 1.0f};
+  }
+  return rgba;
+}
+
+// hash_cell + get_key_from_hash, compute_shader.wgsl:132-142 (u32 wrap).
+__device__ __forceinline__ uint32_t cell_key(int32_t cx, int32_t cy, uint32_t n) {
+  const uint32_t a = (uint32_t)cx * 15823u;
+  const uint32_t b = (uint32_t)cy * 9737333u;
+  return (a + b) % n;
+}
+
+// WGSL i32(f32): truncate toward zero, saturate, NaN -> 0.
+__device__ __forceinline__ int32_t f32_to_i32(float v) {
+  if (v != v) return 0;
+  if (v >= 2147483520.0f) return 2147483647;
+  if (v <= -2147483648.0f) return (int32_t)0x80000000u;
+  return (int32_t)v;
+}
+
+// Sum of attractor accelerations at (x, y), attractors in index order.
+__device__ __forceinline__ void attract(const StreamArgs& a, float x, float y, float& ax,
+                                        float& ay) {
+  float sx = 0.0f, sy = 0.0f;
+#pragma unroll
+  for (int k = 0; k < kMaxAttractors; ++k) {
+    if ((uint32_t)k < a.na) {
+      const float dx = a.ax[k] - x;
+      const float dy = a.ay[k] - y;
+      const float r2 = (dx * dx + dy * dy) + a.ae2[k];
+      const float inv = 1.0f / sqrtf(r2);
+      const float s = a.as[k] * ((inv * inv) * inv);
+      sx = sx + dx * s;
+      sy = sy + dy * s;
+    }
+  }
+  ax = sx;
+  ay = sy;
+}
+
+__device__ __forceinline__ void respawn(const StreamArgs& a, uint64_t gid, float& x, float& y,
+                                     float& vx, float& vy, float& life) {
+  uint32_t w[4];
+  philox4x32_10((uint32_t)gid, (uint32_t)(gid >> 32), a.step_lo, a.step_hi, a.key0, a.key1, w);
+  const float r = a.emit_r * sqrtf(u01(w[0]));
+  float c, s;
+  sincos_turns(u01(w[1]), c, s);
+  x = a.emit_cx + r * c;
+  y = a.emit_cy + r * s;
+  const float spd = a.spd_min + u01(w[3]) * a.spd_range;
+  vx = spd * c;
+  vy = spd * s;
+  life = a.life_min + u01(w[2]) * a.life_range;
+}
+
+// One particle, one active step.  Returns true when the particle respawned.
+template <bool VERLET, bool LIFETIME>
+__device__ __forceinline__ bool step_one(const StreamArgs& a, uint64_t gid, float& x, float& y,
+                                         float& vx, float& vy, float& life) {
+  const float dt = a.dt;
+  if constexpr (!VERLET) {
+    vx = vx + a.gx_dt;  // apply_gravity, wgsl:397-400
+    vy = vy + a.gy_dt;
+    if (a.na) {
+      float ax, ay;
+      attract(a, x, y, ax, ay);
+      vx = vx + ax * dt;
+      vy = vy + ay * dt;
+    }
+    if (a.drag_on) {
+      vx = vx * a.drag_f;
+      vy = vy * a.drag_f;
+    }
+    x = x + vx * dt;  // update_particle_positions, wgsl:392-395
+    y = y + vy * dt;
+  } else {
+    float ax0, ay0, ax1, ay1;
+    attract(a, x, y, ax0, ay0);
+    ay0 = ay0 + a.neg_g;
+    const float x1 = (x + vx * dt) + ax0 * a.half_dt2;
+    const float y1 = (y + vy * dt) + ay0 * a.half_dt2;
+    attract(a, x1, y1, ax1, ay1);
+    ay1 = ay1 + a.neg_g;
+    vx = vx + (ax0 + ax1) * a.half_dt;
+    vy = vy + (ay0 + ay1) * a.half_dt;
+    if (a.drag_on) {
+      vx = vx * a.drag_f;
+      vy = vy * a.drag_f;
+    }
+    x = x1;
+    y = y1;
+  }
+  wall(a.x_min, a.x_max, a.y_min, a.y_max, a.damping, x, y, vx, vy);
+  if constexpr (LIFETIME) {
+    life = life - dt;
+    if (life <= 0.0f) {
+      respawn(a, gid, x, y, vx, vy, life);
+      return true;
+    }
+  }
+  return false;
+}
+
+}  // namespace rps

@@ -1,0 +1,91 @@
+// rps_internal.hpp — launch interface between the C-ABI host code (rps_context.hip) and
+// the gfx950 kernels (rps_kernels.hip).  Not installed; not part of the ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/rps.h"
+#include "rps_device.hpp"
+
+namespace rps {
+
+struct StreamLaunch {
+  int verlet;
+  int lifetime;
+  int stats;
+  int nontemporal;
+  uint32_t grid;  // workgroups (256 threads, 4 particles/thread/iteration)
+};
+
+// Workgroups a one-shot launch of the stream kernel needs for n particles.
+uint32_t stream_blocks_for(uint64_t n);
+
+hipError_t launch_stream_step(const StreamArgs& a, const StreamLaunch& l, hipStream_t s);
+hipError_t launch_stats_finalize(const StatsPartial* partials, uint32_t count,
+                                 StatsResult* out, uint64_t step, hipStream_t s);
+
+hipError_t launch_aos_to_soa(const rps_particle* aos, float* x, float* y, float* vx, float* vy,
+                             uint64_t n, hipStream_t s);
+hipError_t launch_soa_to_aos(const float* x, const float* y, const float* vx, const float* vy,
+                             rps_particle* aos, uint64_t n, float max_energy, int spawn_colour,
+                             hipStream_t s);
+
+struct InitArgs {
+  float* x;
+  float* y;
+  float* vx;
+  float* vy;
+  float* life;  // may be null
+  uint64_t n, id_offset;
+  float x_min, x_max, y_min, y_max, global_count_f, life_min, life_range;
+  uint32_t key0, key1;
+};
+hipError_t launch_init_scatter(const InitArgs& a, hipStream_t s);
+
+// All-pairs N-body.
+constexpr uint32_t kNbodyTile = 512;  // sources staged per LDS tile (float2: 4 KiB)
+hipError_t launch_nbody_pack(const float* x, const float* y, f2* pos, uint64_t n, hipStream_t s);
+hipError_t launch_nbody_pad(f2* pos, uint64_t from, uint64_t to, hipStream_t s);
+hipError_t launch_nbody_accel(const f2* pos, uint64_t ns_padded, uint64_t t0, uint64_t nt,
+                              float eps2, float gm, float* ax, float* ay, hipStream_t s);
+struct NbodyIntegrateArgs {
+  float* x;
+  float* y;
+  float* vx;
+  float* vy;
+  const float* ax;
+  const float* ay;
+  uint64_t n;
+  float dt, gx_dt, gy_dt, drag_f;
+  uint32_t drag_on;
+  float x_min, x_max, y_min, y_max, damping;
+};
+hipError_t launch_nbody_integrate(const NbodyIntegrateArgs& a, hipStream_t s);
+
+// SPH (the reference's five passes).
+struct SphBuffers {
+  const rps_config* cfg;  // device-resident ParticleConfig
+  float* x;
+  float* y;
+  float* vx;    // current velocities (snapshot for neighbours in the sim pass)
+  float* vy;
+  float* vx2;   // sim-pass output velocities (swapped with vx/vy after the pass)
+  float* vy2;
+  uint2* lookup;     // P entries
+  uint32_t* offsets; // N
+  f2* dens;          // N
+  f2* pred;          // N
+  uint32_t n;        // N
+  uint32_t p;        // next_pow2(N)
+};
+hipError_t launch_sph_bin(const SphBuffers& b, hipStream_t s);
+// Runs the whole bitonic network of src/particle_compute.rs:117-149; returns the number of
+// reference passes covered (S(S+1)/2) in *passes.
+hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
+                           uint32_t* launches);
+hipError_t launch_sph_offsets(const SphBuffers& b, hipStream_t s);
+hipError_t launch_sph_pre(const SphBuffers& b, hipStream_t s);
+hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s);
+
+}  // namespace rps

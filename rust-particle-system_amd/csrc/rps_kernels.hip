@@ -1,0 +1,750 @@
+// rps_kernels.hip — hand-written gfx950 kernels for the per-particle step.
+//
+// Reference hot path: ParticleComputeNode::run (src/particle_compute.rs:91-195) dispatching
+// the five WGSL entry points of assets/compute_shader.wgsl.  Layout and roofline of each
+// kernel: DESIGN.md §4-§5.  Built with -ffp-contract=off (see rps_device.hpp).
+#include <hip/hip_runtime.h>
+
+#include "rps_internal.hpp"
+
+namespace rps {
+
+namespace {
+
+constexpr int kBlock = 256;  // 4 waves of 64
+
+template <bool NT>
+__device__ __forceinline__ f4 ld4(const float* p) {
+  if constexpr (NT) {
+    return __builtin_nontemporal_load(reinterpret_cast<const f4*>(p));
+  } else {
+    return *reinterpret_cast<const f4*>(p);
+  }
+}
+
+template <bool NT>
+__device__ __forceinline__ void st4(float* p, f4 v) {
+  if constexpr (NT) {
+    __builtin_nontemporal_store(v, reinterpret_cast<f4*>(p));
+  } else {
+    *reinterpret_cast<f4*>(p) = v;
+  }
+}
+
+struct StatsAcc {
+  float x0, x1, y0, y1;
+  double ke;
+  unsigned long long count, respawned;
+  __device__ void init() {
+    x0 = y0 = __builtin_huge_valf();
+    x1 = y1 = -__builtin_huge_valf();
+    ke = 0.0;
+    count = respawned = 0;
+  }
+  __device__ void add(float x, float y, float vx, float vy, bool re) {
+    x0 = fminf(x0, x);
+    x1 = fmaxf(x1, x);
+    y0 = fminf(y0, y);
+    y1 = fmaxf(y1, y);
+    ke += 0.5 * ((double)vx * (double)vx + (double)vy * (double)vy);
+    count += 1;
+    respawned += re ? 1 : 0;
+  }
+};
+
+// wave64 butterfly reduction, then the 4 waves of the workgroup through LDS; lane 0 of
+// wave 0 writes the workgroup's partial (no atomics: the finalize pass sums partials in a
+// fixed order, so the stats are reproducible run to run).
+__device__ void block_reduce_stats(StatsAcc acc, StatsPartial* out) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    acc.x0 = fminf(acc.x0, __shfl_xor(acc.x0, off, 64));
+    acc.x1 = fmaxf(acc.x1, __shfl_xor(acc.x1, off, 64));
+    acc.y0 = fminf(acc.y0, __shfl_xor(acc.y0, off, 64));
+    acc.y1 = fmaxf(acc.y1, __shfl_xor(acc.y1, off, 64));
+    acc.ke += __shfl_xor(acc.ke, off, 64);
+    acc.count += __shfl_xor(acc.count, off, 64);
+    acc.respawned += __shfl_xor(acc.respawned, off, 64);
+  }
+  __shared__ StatsAcc waves[kBlock / 64];
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) waves[wave] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    StatsAcc t = waves[0];
+#pragma unroll
+    for (int w = 1; w < kBlock / 64; ++w) {
+      t.x0 = fminf(t.x0, waves[w].x0);
+      t.x1 = fmaxf(t.x1, waves[w].x1);
+      t.y0 = fminf(t.y0, waves[w].y0);
+      t.y1 = fmaxf(t.y1, waves[w].y1);
+      t.ke += waves[w].ke;
+      t.count += waves[w].count;
+      t.respawned += waves[w].respawned;
+    }
+    StatsPartial p;
+    p.bbox[0] = t.x0;
+    p.bbox[1] = t.x1;
+    p.bbox[2] = t.y0;
+    p.bbox[3] = t.y1;
+    p.ke = t.ke;
+    p.count = t.count;
+    p.respawned = t.respawned;
+    p._pad = 0;
+    out[blockIdx.x] = p;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Streaming step: one fused pass per active step.  SoA x|y|vx|vy[|life] read and written
+// in place with 16-B vector accesses (4 particles per lane), grid-stride.  40 B/particle
+// with lifetime, 32 B without.
+// ---------------------------------------------------------------------------------------
+template <bool VERLET, bool LIFETIME, bool STATS, bool NT>
+__global__ __launch_bounds__(kBlock) void stream_step_kernel(StreamArgs a) {
+  const uint64_t nvec = a.n >> 2;
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  StatsAcc acc;
+  if constexpr (STATS) acc.init();
+  for (uint64_t v = tid; v < nvec; v += stride) {
+    const uint64_t i = v << 2;
+    f4 X = ld4<NT>(a.x + i);
+    f4 Y = ld4<NT>(a.y + i);
+    f4 VX = ld4<NT>(a.vx + i);
+    f4 VY = ld4<NT>(a.vy + i);
+    f4 L = {0.0f, 0.0f, 0.0f, 0.0f};
+    if constexpr (LIFETIME) L = ld4<NT>(a.life + i);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float x = X[c], y = Y[c], vx = VX[c], vy = VY[c], life = L[c];
+      const bool re = step_one<VERLET, LIFETIME>(a, a.id_offset + i + c, x, y, vx, vy, life);
+      X[c] = x;
+      Y[c] = y;
+      VX[c] = vx;
+      VY[c] = vy;
+      L[c] = life;
+      if constexpr (STATS) acc.add(x, y, vx, vy, re);
+    }
+    st4<NT>(a.x + i, X);
+    st4<NT>(a.y + i, Y);
+    st4<NT>(a.vx + i, VX);
+    st4<NT>(a.vy + i, VY);
+    if constexpr (LIFETIME) st4<NT>(a.life + i, L);
+  }
+  // n % 4 tail particles, one per lane of the first threads.
+  const uint64_t rem = a.n - (nvec << 2);
+  if (tid < rem) {
+    const uint64_t i = (nvec << 2) + tid;
+    float x = a.x[i], y = a.y[i], vx = a.vx[i], vy = a.vy[i];
+    float life = LIFETIME ? a.life[i] : 0.0f;
+    const bool re = step_one<VERLET, LIFETIME>(a, a.id_offset + i, x, y, vx, vy, life);
+    a.x[i] = x;
+    a.y[i] = y;
+    a.vx[i] = vx;
+    a.vy[i] = vy;
+    if constexpr (LIFETIME) a.life[i] = life;
+    if constexpr (STATS) acc.add(x, y, vx, vy, re);
+  }
+  if constexpr (STATS) block_reduce_stats(acc, a.partials);
+}
+
+__global__ __launch_bounds__(kBlock) void stats_finalize_kernel(const StatsPartial* partials,
+                                                                uint32_t count, StatsResult* out,
+                                                                unsigned long long step) {
+  StatsAcc acc;
+  acc.init();
+  for (uint32_t i = threadIdx.x; i < count; i += kBlock) {
+    const StatsPartial p = partials[i];
+    acc.x0 = fminf(acc.x0, p.bbox[0]);
+    acc.x1 = fmaxf(acc.x1, p.bbox[1]);
+    acc.y0 = fminf(acc.y0, p.bbox[2]);
+    acc.y1 = fmaxf(acc.y1, p.bbox[3]);
+    acc.ke += p.ke;
+    acc.count += p.count;
+    acc.respawned += p.respawned;
+  }
+  __shared__ StatsPartial res[1];
+  block_reduce_stats(acc, res - blockIdx.x);  // writes res[0]
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    StatsResult r;
+    for (int k = 0; k < 4; ++k) r.bbox[k] = res[0].bbox[k];
+    r.ke = res[0].ke;
+    r.count = res[0].count;
+    r.respawned = res[0].respawned;
+    r.step = step;
+    *out = r;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// AoS <-> SoA (the 32-B Particle of src/particle.rs:20-25)
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void aos_to_soa_kernel(const rps_particle* aos, float* x,
+                                                            float* y, float* vx, float* vy,
+                                                            uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const f4 pv = *reinterpret_cast<const f4*>(&aos[i].position[0]);
+  x[i] = pv[0];
+  y[i] = pv[1];
+  vx[i] = pv[2];
+  vy[i] = pv[3];
+}
+
+__global__ __launch_bounds__(kBlock) void soa_to_aos_kernel(const float* x, const float* y,
+                                                            const float* vx, const float* vy,
+                                                            rps_particle* aos, uint64_t n,
+                                                            float max_energy, int spawn_colour) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const float qx = vx[i], qy = vy[i];
+  *reinterpret_cast<f4*>(&aos[i].position[0]) = f4{x[i], y[i], qx, qy};
+  const f4 c = spawn_colour ? f4{1.0f, 1.0f, 1.0f, 1.0f} : set_color(qx, qy, max_energy);
+  *reinterpret_cast<f4*>(&aos[i].color[0]) = c;
+}
+
+// ---------------------------------------------------------------------------------------
+// Initial scatter (seeded restatement of src/main.rs:182-216)
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void init_scatter_kernel(InitArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= a.n) return;
+  const uint64_t g = a.id_offset + i;
+  const float t = (float)g / a.global_count_f;
+  a.x[i] = a.x_min + t * (a.x_max - a.x_min);
+  uint32_t w[4];
+  philox4x32_10((uint32_t)g, (uint32_t)(g >> 32), 0xFFFFFFFFu, 0xFFFFFFFFu, a.key0, a.key1, w);
+  const float u1 = (float)((w[0] >> 8) + 1u) * (1.0f / 16777216.0f);
+  float c, s;
+  sincos_turns(u01(w[1]), c, s);
+  const float z = sqrtf(-2.0f * logf(u1)) * c;
+  const float y_center = (a.y_min + a.y_max) / 2.0f;
+  const float y_sd = (a.y_max - a.y_min) * 0.125f;
+  float yy = y_center + z * y_sd;
+  yy = yy < a.y_min ? a.y_min : yy;
+  yy = yy > a.y_max ? a.y_max : yy;
+  a.y[i] = yy;
+  a.vx[i] = 0.0f;
+  a.vy[i] = 0.0f;
+  if (a.life) a.life[i] = a.life_min + u01(w[2]) * a.life_range;
+}
+
+// ---------------------------------------------------------------------------------------
+// All-pairs N-body: float2 source tiles staged through LDS, 4 targets per lane in
+// registers, v_rsq_f32 + FMA inner loop.  FP32-VALU bound.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void nbody_pack_kernel(const float* x, const float* y,
+                                                            f2* pos, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i < n) pos[i] = f2{x[i], y[i]};
+}
+
+__global__ __launch_bounds__(kBlock) void nbody_pad_kernel(f2* pos, uint64_t from, uint64_t to) {
+  const uint64_t i = from + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  // Far-away padding: r2 = 2e36 -> inv^3 underflows to 0, so a pad adds exactly +0.
+  if (i < to) pos[i] = f2{1.0e18f, 1.0e18f};
+}
+
+constexpr int kTargetsPerLane = 4;
+
+__global__ __launch_bounds__(kBlock) void nbody_accel_kernel(const f2* __restrict__ pos,
+                                                             uint64_t ns_padded, uint64_t t0,
+                                                             uint64_t nt, float eps2, float gm,
+                                                             float* __restrict__ ax_out,
+                                                             float* __restrict__ ay_out) {
+  __shared__ f4 tile[kNbodyTile / 2];  // pairs of float2 sources
+  const uint64_t base = (uint64_t)blockIdx.x * kBlock * kTargetsPerLane;
+  float tx[kTargetsPerLane], ty[kTargetsPerLane], ax[kTargetsPerLane], ay[kTargetsPerLane];
+#pragma unroll
+  for (int k = 0; k < kTargetsPerLane; ++k) {
+    const uint64_t t = base + threadIdx.x + (uint64_t)k * kBlock;
+    const f2 p = t < nt ? pos[t0 + t] : f2{0.0f, 0.0f};
+    tx[k] = p[0];
+    ty[k] = p[1];
+    ax[k] = 0.0f;
+    ay[k] = 0.0f;
+  }
+  const f4* src4 = reinterpret_cast<const f4*>(pos);
+  for (uint64_t s0 = 0; s0 < ns_padded; s0 += kNbodyTile) {
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < kNbodyTile / 2; q += kBlock) tile[q] = src4[(s0 >> 1) + q];
+    __syncthreads();
+#pragma unroll 4
+    for (uint32_t q = 0; q < kNbodyTile / 2; ++q) {
+      const f4 sp = tile[q];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float sx = sp[2 * h], sy = sp[2 * h + 1];
+#pragma unroll
+        for (int k = 0; k < kTargetsPerLane; ++k) {
+          const float dx = sx - tx[k];
+          const float dy = sy - ty[k];
+          const float r2 = __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, eps2));
+          const float inv = __builtin_amdgcn_rsqf(r2);
+          const float inv3 = (inv * inv) * inv;
+          ax[k] = __builtin_fmaf(dx, inv3, ax[k]);
+          ay[k] = __builtin_fmaf(dy, inv3, ay[k]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kTargetsPerLane; ++k) {
+    const uint64_t t = base + threadIdx.x + (uint64_t)k * kBlock;
+    if (t < nt) {
+      ax_out[t] = ax[k] * gm;
+      ay_out[t] = ay[k] * gm;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void nbody_integrate_kernel(NbodyIntegrateArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= a.n) return;
+  float px = a.x[i], py = a.y[i], qx = a.vx[i], qy = a.vy[i];
+  qx = qx + a.gx_dt;
+  qy = qy + a.gy_dt;
+  qx = qx + a.ax[i] * a.dt;
+  qy = qy + a.ay[i] * a.dt;
+  if (a.drag_on) {
+    qx = qx * a.drag_f;
+    qy = qy * a.drag_f;
+  }
+  px = px + qx * a.dt;
+  py = py + qy * a.dt;
+  wall(a.x_min, a.x_max, a.y_min, a.y_max, a.damping, px, py, qx, qy);
+  a.x[i] = px;
+  a.y[i] = py;
+  a.vx[i] = qx;
+  a.vy[i] = qy;
+}
+
+// ---------------------------------------------------------------------------------------
+// SPH: the reference's five passes
+// ---------------------------------------------------------------------------------------
+
+// bin_particles_in_grid, compute_shader.wgsl:455-468 (+ :121-142).
+__global__ __launch_bounds__(kBlock) void sph_bin_kernel(const rps_config* __restrict__ cfg,
+                                                         const float* __restrict__ x,
+                                                         const float* __restrict__ y,
+                                                         uint2* __restrict__ lookup,
+                                                         uint32_t* __restrict__ offsets,
+                                                         uint32_t n) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const float r = cfg->smoothing_radius;
+  const int32_t cx = f32_to_i32((x[i] + cfg->screen_bounds[1]) / r);
+  const int32_t cy = f32_to_i32((y[i] + cfg->screen_bounds[3]) / r);
+  lookup[i] = make_uint2(cell_key(cx, cy, cfg->particle_count), i);
+  offsets[i] = 0xFFFFFFFFu;
+}
+
+// sort_particles, compute_shader.wgsl:470-505: one compare-swap of pair i of the pass
+// (group_width gw; flip = step_index == 0).
+__device__ __forceinline__ void bitonic_pair(uint32_t i, uint32_t gw, bool flip, uint32_t& left,
+                                             uint32_t& right) {
+  const uint32_t gh = 2u * gw - 1u;
+  const uint32_t h = i & (gw - 1u);
+  left = h + (gh + 1u) * (i / gw);
+  right = left + (flip ? gh - 2u * h : (gh + 1u) / 2u);
+}
+
+// One global pass (group_width >= LDS tile): P/2 threads.
+__global__ __launch_bounds__(kBlock) void sph_sort_global_kernel(uint2* __restrict__ lookup,
+                                                                 uint32_t p, uint32_t gw,
+                                                                 uint32_t flip) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= p / 2u) return;
+  uint32_t l, r;
+  bitonic_pair(i, gw, flip != 0, l, r);
+  if (r >= p) return;
+  const uint2 a = lookup[l], b = lookup[r];
+  if (a.x > b.x) {
+    lookup[l] = b;
+    lookup[r] = a;
+  }
+}
+
+constexpr uint32_t kSortTile = 2048;  // entries per workgroup tile (16 KiB of LDS)
+
+// Every remaining pass of stages [stage_lo, stage_hi] whose group_width fits one tile:
+// a pass with 2*gw <= tile only pairs entries inside aligned blocks of 2*gw, so a tile of
+// the array can run it on its own.  Same network, same compare order per pair -> identical
+// result to the reference's pass-per-dispatch schedule.
+__global__ __launch_bounds__(1024) void sph_sort_local_kernel(uint2* __restrict__ lookup,
+                                                              uint32_t tile, uint32_t stage_lo,
+                                                              uint32_t stage_hi,
+                                                              uint32_t first_step) {
+  __shared__ uint2 s[kSortTile];
+  const uint32_t base = blockIdx.x * tile;
+  for (uint32_t q = threadIdx.x; q < tile; q += blockDim.x) s[q] = lookup[base + q];
+  __syncthreads();
+  for (uint32_t stage = stage_lo; stage <= stage_hi; ++stage) {
+    for (uint32_t step = (stage == stage_lo ? first_step : 0u); step <= stage; ++step) {
+      const uint32_t gw = 1u << (stage - step);
+      for (uint32_t i = threadIdx.x; i < tile / 2u; i += blockDim.x) {
+        uint32_t l, r;
+        bitonic_pair(i, gw, step == 0u, l, r);
+        const uint2 a = s[l], b = s[r];
+        if (a.x > b.x) {
+          s[l] = b;
+          s[r] = a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (uint32_t q = threadIdx.x; q < tile; q += blockDim.x) lookup[base + q] = s[q];
+}
+
+// calculate_spatial_lookup_offsets, compute_shader.wgsl:507-525.
+__global__ __launch_bounds__(kBlock) void sph_offsets_kernel(const uint2* __restrict__ lookup,
+                                                             uint32_t* __restrict__ offsets,
+                                                             uint32_t n) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t key = lookup[i].x;
+  const uint32_t prev = i > 0u ? lookup[i - 1u].x : 0xFFFFFFFFu;
+  if (key != prev) offsets[key] = i;
+}
+
+// pre_simulation_step part 1 (wgsl:397-405): gravity + predicted position for all
+// particles, so the density pass reads a complete snapshot.
+__global__ __launch_bounds__(kBlock) void sph_predict_kernel(const rps_config* __restrict__ cfg,
+                                                             const float* __restrict__ x,
+                                                             const float* __restrict__ y,
+                                                             float* __restrict__ vx,
+                                                             float* __restrict__ vy,
+                                                             f2* __restrict__ pred, uint32_t n) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const float dt = cfg->fixed_delta_time;
+  const float qx = vx[i] + 0.0f * dt;
+  const float qy = vy[i] + (-cfg->gravity) * dt;
+  vx[i] = qx;
+  vy[i] = qy;
+  pred[i] = f2{x[i] + qx * dt, y[i] + qy * dt};
+}
+
+__constant__ int32_t kGridOff[9][2] = {{-1, -1}, {-1, 0}, {-1, 1}, {0, -1}, {0, 0},
+                                       {0, 1},   {1, -1}, {1, 0},  {1, 1}};
+
+// calculate_density, compute_shader.wgsl:207-254.
+__global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* __restrict__ cfg,
+                                                             const uint2* __restrict__ lookup,
+                                                             const uint32_t* __restrict__ offsets,
+                                                             const f2* __restrict__ pred,
+                                                             f2* __restrict__ dens, uint32_t n) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const float r = cfg->smoothing_radius, r2 = r * r;
+  const uint32_t N = cfg->particle_count;
+  const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
+  const f2 p = pred[i];
+  const int32_t cx = f32_to_i32((p[0] + cfg->screen_bounds[1]) / r);
+  const int32_t cy = f32_to_i32((p[1] + cfg->screen_bounds[3]) / r);
+  float d = 0.0f, nd = 0.0f;
+  for (int o = 0; o < 9; ++o) {
+    const uint32_t key = cell_key((int32_t)((uint32_t)cx + (uint32_t)kGridOff[o][0]),
+                                  (int32_t)((uint32_t)cy + (uint32_t)kGridOff[o][1]), N);
+    for (uint32_t j = offsets[key]; j < N; ++j) {
+      const uint2 e = lookup[j];
+      if (e.x != key) break;
+      const f2 q = pred[e.y];
+      const float dx = p[0] - q[0], dy = p[1] - q[1];
+      const float sq = dx * dx + dy * dy;
+      if (sq > r2) continue;
+      const float dist = sqrtf(sq);
+      float k1 = 0.0f, k2 = 0.0f;
+      if (!(dist >= r)) {
+        const float v = r - dist;
+        k1 = (dn * v) * v;
+        k2 = ((ndn * v) * v) * v;
+      }
+      d = d + k1;
+      nd = nd + k2;
+    }
+  }
+  dens[i] = f2{d, nd};
+}
+
+// simulation_step, compute_shader.wgsl:435-453: pressure (:256-334) and viscosity
+// (:336-384) against the start-of-pass velocity snapshot (vx, vy), Euler (:392-395) and
+// walls (:69-99).  New velocities go to (vx2, vy2); positions update in place.
+__global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __restrict__ cfg,
+                                                         const uint2* __restrict__ lookup,
+                                                         const uint32_t* __restrict__ offsets,
+                                                         const f2* __restrict__ pred,
+                                                         const f2* __restrict__ dens,
+                                                         const float* __restrict__ vx,
+                                                         const float* __restrict__ vy,
+                                                         float* __restrict__ vx2,
+                                                         float* __restrict__ vy2,
+                                                         float* __restrict__ x,
+                                                         float* __restrict__ y, uint32_t n) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const float dt = cfg->fixed_delta_time;
+  const float r = cfg->smoothing_radius, r2 = r * r;
+  const uint32_t N = cfg->particle_count;
+  const float td = cfg->target_density, pm = cfg->pressure_multiplier;
+  const float nm = cfg->near_density_multiplier;
+  const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
+  const float vn = cfg->viscocity_kernel_norm;
+  const f2 p = pred[i];
+  const int32_t cx = f32_to_i32((p[0] + cfg->screen_bounds[1]) / r);
+  const int32_t cy = f32_to_i32((p[1] + cfg->screen_bounds[3]) / r);
+  const f2 rr = dens[i];
+  const float rho = rr[0], rhon = rr[1];
+  const float P = (rho - td) * pm;
+  const float Pn = rhon * nm;
+  float fx = 0.0f, fy = 0.0f;
+  for (int o = 0; o < 9; ++o) {
+    const uint32_t key = cell_key((int32_t)((uint32_t)cx + (uint32_t)kGridOff[o][0]),
+                                  (int32_t)((uint32_t)cy + (uint32_t)kGridOff[o][1]), N);
+    for (uint32_t j = offsets[key]; j < N; ++j) {
+      const uint2 e = lookup[j];
+      if (e.x != key) break;
+      if (e.y == i) continue;
+      const f2 q = pred[e.y];
+      const float dx = q[0] - p[0], dy = q[1] - p[1];
+      const float sq = dx * dx + dy * dy;
+      if (sq > r2) continue;
+      const float dist = sqrtf(sq);
+      float dirx, diry;
+      if (dist > 0.0001f) {
+        dirx = dx / dist;
+        diry = dy / dist;
+      } else {
+        dirx = 0.0f;
+        diry = 1.0f;
+      }
+      const f2 dj = dens[e.y];
+      const float rj = dj[0], rnj = dj[1];
+      const float Pj = (rj - td) * pm;
+      const float Pnj = rnj * nm;
+      const float pt = (P / (rho * rho)) + (Pj / (rj * rj));
+      const float npt = (Pn / (rho * rho)) + (Pnj / (rj * rnj));
+      float dk = 0.0f, ndk = 0.0f;
+      if (!(dist >= r)) {
+        const float v = r - dist;
+        dk = (-2.0f * dn) * v;
+        ndk = ((-3.0f * ndn) * v) * v;
+      }
+      fx = fx + (dirx * pt) * dk;
+      fy = fy + (diry * pt) * dk;
+      fx = fx + (dirx * npt) * ndk;
+      fy = fy + (diry * npt) * ndk;
+    }
+  }
+  float qx = vx[i] + fx * dt;
+  float qy = vy[i] + fy * dt;
+  float wx = 0.0f, wy = 0.0f;
+  for (int o = 0; o < 9; ++o) {
+    const uint32_t key = cell_key((int32_t)((uint32_t)cx + (uint32_t)kGridOff[o][0]),
+                                  (int32_t)((uint32_t)cy + (uint32_t)kGridOff[o][1]), N);
+    for (uint32_t j = offsets[key]; j < N; ++j) {
+      const uint2 e = lookup[j];
+      if (e.x != key) break;
+      if (e.y == i) continue;
+      const f2 q = pred[e.y];
+      const float dx = p[0] - q[0], dy = p[1] - q[1];
+      const float sq = dx * dx + dy * dy;
+      if (sq > r2) continue;
+      const float dist = sqrtf(sq);
+      float k = 0.0f;
+      if (!(dist >= r)) {
+        const float v = r * r - dist * dist;
+        k = ((vn * v) * v) * v;
+      }
+      wx = wx + (vx[e.y] - qx) * k;
+      wy = wy + (vy[e.y] - qy) * k;
+    }
+  }
+  qx = qx + (wx * cfg->viscocity_strength) * dt;
+  qy = qy + (wy * cfg->viscocity_strength) * dt;
+  float ox = x[i] + qx * dt;
+  float oy = y[i] + qy * dt;
+  wall(cfg->screen_bounds[0], cfg->screen_bounds[1], cfg->screen_bounds[2], cfg->screen_bounds[3],
+       cfg->damping_factor, ox, oy, qx, qy);
+  x[i] = ox;
+  y[i] = oy;
+  vx2[i] = qx;
+  vy2[i] = qy;
+}
+
+inline uint32_t blocks_for(uint64_t n, uint32_t per_block = kBlock) {
+  return (uint32_t)((n + per_block - 1) / per_block);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------
+// Launchers
+// ---------------------------------------------------------------------------------------
+uint32_t stream_blocks_for(uint64_t n) {
+  const uint64_t nvec = n >> 2;
+  uint64_t b = (nvec + kBlock - 1) / kBlock;
+  if (b == 0) b = 1;
+  return (uint32_t)(b > 0x7FFFFFFFull ? 0x7FFFFFFFull : b);
+}
+
+template <bool V, bool L, bool S, bool NT>
+static hipError_t launch_stream_t(const StreamArgs& a, uint32_t grid, hipStream_t s) {
+  hipLaunchKernelGGL((stream_step_kernel<V, L, S, NT>), dim3(grid), dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_stream_step(const StreamArgs& a, const StreamLaunch& l, hipStream_t s) {
+  const int sel = (l.verlet ? 8 : 0) | (l.lifetime ? 4 : 0) | (l.stats ? 2 : 0) | (l.nontemporal ? 1 : 0);
+  switch (sel) {
+    case 0: return launch_stream_t<false, false, false, false>(a, l.grid, s);
+    case 1: return launch_stream_t<false, false, false, true>(a, l.grid, s);
+    case 2: return launch_stream_t<false, false, true, false>(a, l.grid, s);
+    case 3: return launch_stream_t<false, false, true, true>(a, l.grid, s);
+    case 4: return launch_stream_t<false, true, false, false>(a, l.grid, s);
+    case 5: return launch_stream_t<false, true, false, true>(a, l.grid, s);
+    case 6: return launch_stream_t<false, true, true, false>(a, l.grid, s);
+    case 7: return launch_stream_t<false, true, true, true>(a, l.grid, s);
+    case 8: return launch_stream_t<true, false, false, false>(a, l.grid, s);
+    case 9: return launch_stream_t<true, false, false, true>(a, l.grid, s);
+    case 10: return launch_stream_t<true, false, true, false>(a, l.grid, s);
+    case 11: return launch_stream_t<true, false, true, true>(a, l.grid, s);
+    case 12: return launch_stream_t<true, true, false, false>(a, l.grid, s);
+    case 13: return launch_stream_t<true, true, false, true>(a, l.grid, s);
+    case 14: return launch_stream_t<true, true, true, false>(a, l.grid, s);
+    default: return launch_stream_t<true, true, true, true>(a, l.grid, s);
+  }
+}
+
+hipError_t launch_stats_finalize(const StatsPartial* partials, uint32_t count, StatsResult* out,
+                                 uint64_t step, hipStream_t s) {
+  hipLaunchKernelGGL(stats_finalize_kernel, dim3(1), dim3(kBlock), 0, s, partials, count, out,
+                     (unsigned long long)step);
+  return hipGetLastError();
+}
+
+hipError_t launch_aos_to_soa(const rps_particle* aos, float* x, float* y, float* vx, float* vy,
+                             uint64_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(aos_to_soa_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, s, aos, x, y, vx,
+                     vy, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_soa_to_aos(const float* x, const float* y, const float* vx, const float* vy,
+                             rps_particle* aos, uint64_t n, float max_energy, int spawn_colour,
+                             hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(soa_to_aos_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, s, x, y, vx, vy,
+                     aos, n, max_energy, spawn_colour);
+  return hipGetLastError();
+}
+
+hipError_t launch_init_scatter(const InitArgs& a, hipStream_t s) {
+  if (a.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(init_scatter_kernel, dim3(blocks_for(a.n)), dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_nbody_pack(const float* x, const float* y, f2* pos, uint64_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(nbody_pack_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, s, x, y, pos, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_nbody_pad(f2* pos, uint64_t from, uint64_t to, hipStream_t s) {
+  if (to <= from) return hipSuccess;
+  hipLaunchKernelGGL(nbody_pad_kernel, dim3(blocks_for(to - from)), dim3(kBlock), 0, s, pos, from,
+                     to);
+  return hipGetLastError();
+}
+
+hipError_t launch_nbody_accel(const f2* pos, uint64_t ns_padded, uint64_t t0, uint64_t nt,
+                              float eps2, float gm, float* ax, float* ay, hipStream_t s) {
+  if (nt == 0) return hipSuccess;
+  hipLaunchKernelGGL(nbody_accel_kernel, dim3(blocks_for(nt, kBlock * kTargetsPerLane)),
+                     dim3(kBlock), 0, s, pos, ns_padded, t0, nt, eps2, gm, ax, ay);
+  return hipGetLastError();
+}
+
+hipError_t launch_nbody_integrate(const NbodyIntegrateArgs& a, hipStream_t s) {
+  if (a.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(nbody_integrate_kernel, dim3(blocks_for(a.n)), dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_sph_bin(const SphBuffers& b, hipStream_t s) {
+  hipLaunchKernelGGL(sph_bin_kernel, dim3(blocks_for(b.n)), dim3(kBlock), 0, s, b.cfg, b.x, b.y,
+                     b.lookup, b.offsets, b.n);
+  return hipGetLastError();
+}
+
+hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
+                           uint32_t* launches) {
+  const uint32_t P = b.p;
+  uint32_t stages = 0;
+  while ((1u << stages) < P) ++stages;
+  *passes = stages * (stages + 1u) / 2u;
+  *launches = 0;
+  if (stages == 0) return hipSuccess;
+  const uint32_t tile = P < kSortTile ? P : kSortTile;
+  uint32_t tile_log = 0;
+  while ((1u << tile_log) < tile) ++tile_log;
+  const uint32_t local_threads = tile / 2u < 1024u ? tile / 2u : 1024u;
+  const uint32_t tiles = P / tile;
+  // Stages whose whole network fits one tile: one launch.
+  const uint32_t first_global_stage = tile_log;  // stage s has 2*2^s = 2^(s+1) span
+  hipLaunchKernelGGL(sph_sort_local_kernel, dim3(tiles), dim3(local_threads), 0, s, b.lookup,
+                     tile, 0u, first_global_stage - 1u, 0u);
+  ++*launches;
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  for (uint32_t stage = first_global_stage; stage < stages; ++stage) {
+    uint32_t step = 0;
+    // Passes whose compare span 2*gw exceeds the tile run as global passes.
+    for (; step <= stage; ++step) {
+      const uint32_t gw = 1u << (stage - step);
+      if (2u * gw <= tile) break;
+      hipLaunchKernelGGL(sph_sort_global_kernel, dim3(blocks_for(P / 2u)), dim3(kBlock), 0, s,
+                         b.lookup, P, gw, step == 0u ? 1u : 0u);
+      ++*launches;
+      e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+    if (step <= stage) {
+      hipLaunchKernelGGL(sph_sort_local_kernel, dim3(tiles), dim3(local_threads), 0, s, b.lookup,
+                         tile, stage, stage, step);
+      ++*launches;
+      e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+  }
+  return hipSuccess;
+}
+
+hipError_t launch_sph_offsets(const SphBuffers& b, hipStream_t s) {
+  hipLaunchKernelGGL(sph_offsets_kernel, dim3(blocks_for(b.n)), dim3(kBlock), 0, s, b.lookup,
+                     b.offsets, b.n);
+  return hipGetLastError();
+}
+
+hipError_t launch_sph_pre(const SphBuffers& b, hipStream_t s) {
+  hipLaunchKernelGGL(sph_predict_kernel, dim3(blocks_for(b.n)), dim3(kBlock), 0, s, b.cfg, b.x,
+                     b.y, b.vx, b.vy, b.pred, b.n);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(sph_density_kernel, dim3(blocks_for(b.n)), dim3(kBlock), 0, s, b.cfg,
+                     b.lookup, b.offsets, b.pred, b.dens, b.n);
+  return hipGetLastError();
+}
+
+hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s) {
+  hipLaunchKernelGGL(sph_sim_kernel, dim3(blocks_for(b.n)), dim3(kBlock), 0, s, b.cfg, b.lookup,
+                     b.offsets, b.pred, b.dens, b.vx, b.vy, b.vx2, b.vy2, b.x, b.y, b.n);
+  return hipGetLastError();
+}
+
+}  // namespace rps

@@ -1,0 +1,85 @@
+"""The C-ABI library loads and exports every symbol include/rps.h declares; struct layouts
+match the header (no compute calls: runs without a GPU)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "rps.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(rps_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_expected_surface():
+    names = declared_functions()
+    for must in ("rps_create", "rps_set_config", "rps_upload_particles", "rps_step",
+                 "rps_download_particles", "rps_read_debug", "rps_get_stats", "rps_comm_init"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol(rps):
+    L = rps.lib()
+    missing = [n for n in declared_functions() if not hasattr(L, n)]
+    assert not missing, missing
+    bound = {name for name, _, _ in rps.ABI_SYMBOLS}
+    assert bound == set(declared_functions()), "python binding out of sync with rps.h"
+
+
+def test_exports_are_c_linkage(rps):
+    out = subprocess.run(["nm", "-D", "--defined-only", rps.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT (rps_[a-z0-9_]+)\b", out))
+    assert set(declared_functions()) <= exported
+
+
+def test_struct_layouts(rps):
+    assert ctypes.sizeof(rps.ParticleConfig) == 144  # src/main.rs:43-69
+    assert rps.ParticleConfig.screen_bounds.offset == 64
+    assert rps.ParticleConfig.view_proj.offset == 80
+    assert rps.ParticleConfig.frame_count.offset == 24
+    assert rps.PARTICLE_DTYPE.itemsize == 32  # src/particle.rs:20-25
+    assert rps.PARTICLE_DTYPE.fields["velocity"][1] == 8
+    assert rps.PARTICLE_DTYPE.fields["color"][1] == 16
+    assert ctypes.sizeof(rps.Attractor) == 32
+    assert ctypes.sizeof(rps.ExtConfig) == 72 + 8 * 32
+
+
+def test_c_header_compiles_and_sizes_agree(tmp_path):
+    prog = tmp_path / "sz.c"
+    prog.write_text('#include "rps.h"\n#include <stdio.h>\n#include <stddef.h>\n'
+                    'int main(void){printf("%zu %zu %zu %zu %zu\\n", sizeof(rps_config), '
+                    'sizeof(rps_particle), sizeof(rps_ext_config), offsetof(rps_config, screen_bounds),'
+                    ' sizeof(rps_stats));return 0;}\n')
+    exe = tmp_path / "sz"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    str(prog), "-o", str(exe)], check=True)
+    got = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
+    assert got == ["144", "32", "328", "64", "48"]
+
+
+def test_status_strings_and_null_handling(rps):
+    L = rps.lib()
+    assert L.rps_abi_version() == 1
+    assert L.rps_status_string(0) == b"ok"
+    assert L.rps_status_string(4) == b"unsupported"
+    # null arguments are rejected without touching the device
+    assert L.rps_create(None, None) == rps.RPS_ERR_INVALID_ARGUMENT
+    assert L.rps_step(None, 1) == rps.RPS_ERR_INVALID_ARGUMENT
+    assert b"null" in L.rps_last_error(None)
+    assert L.rps_destroy(None) == 0
+
+
+def test_no_cpu_fallback_when_library_missing(monkeypatch, rps):
+    import importlib
+
+    monkeypatch.setattr(rps, "LIB_PATH", "/nonexistent/librps.so")
+    monkeypatch.setattr(rps, "_lib", None)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        rps.lib()

@@ -1,0 +1,228 @@
+"""GPU parity of the streaming step (mode STREAM) against the CPU oracle, through the C ABI.
+
+Bar: bitwise for every field (x, y, vx, vy, life), every step — the kernels and the oracle
+both compute IEEE f32 with no contraction and correctly-rounded div/sqrt."""
+import numpy as np
+import pytest
+
+from helpers import (F, assert_bitwise, assert_soa_bitwise, config_c1, copy_soa, ext_verlet_1att,
+                     random_soa, soa_to_particles)
+
+pytestmark = pytest.mark.gpu
+
+KEYS5 = ("x", "y", "vx", "vy", "life")
+
+
+def _gpu_ctx(rps, n, cfg, ext, soa, id_offset=0, global_count=0):
+    ctx = rps.Context(n, rps.MODE_STREAM, id_offset=id_offset, global_count=global_count)
+    ctx.set_config(cfg, ext)
+    ctx.upload_soa(soa)
+    return ctx
+
+
+def test_c1_reference_subset_with_shader_delay(gpu, orc):
+    """C1: 65 536 particles, reference scatter, gravity + Euler + walls, SHADER_DELAY 5."""
+    rps = gpu
+    n = 65536
+    cfg = config_c1(rps, n, gravity=9.8)
+    ext = rps.make_ext()  # reference semantics
+    parts = rps.setup_particles_scatter(cfg, n, seed=7)
+    with rps.Context(n) as ctx:
+        ctx.set_config(cfg, ext)
+        ctx.upload(parts)
+        got0 = ctx.download()
+        assert np.array_equal(got0["color"], np.ones((n, 4), F))  # spawn colour before stepping
+        assert_bitwise(got0["position"].reshape(-1), parts["position"].reshape(-1), "upload")
+        soa = dict(x=parts["position"][:, 0].copy(), y=parts["position"][:, 1].copy(),
+                   vx=parts["velocity"][:, 0].copy(), vy=parts["velocity"][:, 1].copy())
+        ctx.step(4)
+        assert ctx.counters() == (4, 0)
+        assert_soa_bitwise(ctx.download_soa(), soa, what="gated ")
+        ctx.step(60)
+        fc, act = orc.run_steps(0, cfg, ext, soa, 64)
+        assert ctx.counters() == (fc, act) == (64, 60)
+        got = ctx.download_soa()
+        assert_soa_bitwise(got, soa)
+        aos = ctx.download()
+        want_c = orc.set_color_array(soa["vx"], soa["vy"], cfg.max_energy)
+        assert_bitwise(aos["color"].reshape(-1), want_c.reshape(-1), "colour")
+
+
+def test_c2_verlet_one_attractor(gpu, orc):
+    """C2: 2^20 particles, one attractor, velocity-Verlet fp32; device-side initial scatter."""
+    rps = gpu
+    n = 1 << 20
+    cfg = config_c1(rps, n, gravity=0.0)
+    ext = ext_verlet_1att(rps)
+    with rps.Context(n) as ctx:
+        ctx.set_config(cfg, ext)
+        ctx.init_scatter(seed=0x5EED)
+        soa = ctx.download_soa()
+        for s in range(3):
+            ctx.step(1)
+            orc.stream_step(cfg, ext, soa, s)
+            assert_soa_bitwise(ctx.download_soa(), soa, what=f"step{s} ")
+
+
+def test_headline_features_bitwise(gpu, orc):
+    """C3 features (4 moving attractors, drag, lifetime, Philox respawn) at 2^20, 25 steps."""
+    rps = gpu
+    n = 1 << 20
+    cfg = config_c1(rps, n)
+    ext = rps.headline_ext()
+    ext.shader_delay = 0
+    soa = random_soa(n, list(cfg.screen_bounds), seed=21, life=(-0.05, 0.3))
+    with _gpu_ctx(rps, n, cfg, ext, soa) as ctx:
+        ref = copy_soa(soa)
+        for s in range(25):
+            orc.stream_step(cfg, ext, ref, s)
+        ctx.step(25)
+        assert_soa_bitwise(ctx.download_soa(life=True), ref, keys=KEYS5)
+
+
+@pytest.mark.parametrize("n", [1, 3, 5, 63, 1023, 4097, 65539])
+def test_ragged_sizes(gpu, orc, n):
+    rps = gpu
+    cfg = config_c1(rps, n)
+    ext = rps.headline_ext()
+    ext.shader_delay = 0
+    soa = random_soa(n, list(cfg.screen_bounds), seed=n, life=(-0.05, 0.2))
+    with _gpu_ctx(rps, n, cfg, ext, soa) as ctx:
+        ref = copy_soa(soa)
+        for s in range(5):
+            orc.stream_step(cfg, ext, ref, s)
+        ctx.step(5)
+        assert_soa_bitwise(ctx.download_soa(life=True), ref, keys=KEYS5)
+
+
+def test_sharded_contexts_use_global_ids(gpu, orc):
+    """A rank's shard (id_offset, global_count) equals the matching slice of the whole."""
+    rps = gpu
+    n, shard = 40000, 10000
+    cfg = config_c1(rps, n)
+    ext = rps.headline_ext()
+    ext.shader_delay = 0
+    soa = random_soa(n, list(cfg.screen_bounds), seed=31, life=(-0.1, 0.4))
+    whole = copy_soa(soa)
+    for s in range(6):
+        orc.stream_step(cfg, ext, whole, s)
+    for r in range(4):
+        lo = r * shard
+        part = {k: v[lo:lo + shard].copy() for k, v in soa.items()}
+        with _gpu_ctx(rps, shard, cfg, ext, part, id_offset=lo, global_count=n) as ctx:
+            ctx.step(6)
+            got = ctx.download_soa(life=True)
+        for k in KEYS5:
+            assert_bitwise(got[k], whole[k][lo:lo + shard], f"rank{r} {k}")
+
+
+def test_stats_reduction(gpu, orc):
+    rps = gpu
+    n = 300001
+    cfg = config_c1(rps, n)
+    ext = rps.headline_ext(stats=True)
+    ext.shader_delay = 0
+    ext.stats_interval = 1
+    soa = random_soa(n, list(cfg.screen_bounds), seed=41, life=(-0.02, 0.5))
+    with _gpu_ctx(rps, n, cfg, ext, soa) as ctx:
+        ctx.step(1)
+        st = ctx.stats()
+    ref = copy_soa(soa)
+    ost = orc.stream_step(cfg, ext, ref, 0, stats=True)
+    assert st.particles == n and st.step == 0
+    assert st.respawned == ost.respawned > 0
+    assert list(st.bbox) == list(ost.bbox)
+    assert abs(st.kinetic_energy - ost.kinetic_energy) <= 1e-9 * abs(ost.kinetic_energy)
+
+
+def test_init_scatter_matches_oracle(gpu, orc):
+    rps = gpu
+    n = 100000
+    cfg = config_c1(rps, n)
+    ext = rps.headline_ext()
+    with rps.Context(n, id_offset=5000, global_count=200000) as ctx:
+        ctx.set_config(cfg, ext)
+        ctx.init_scatter(seed=99)
+        got = ctx.download_soa(life=True)
+    want = orc.init_scatter(cfg, ext, 99, n, id_offset=5000, global_count=200000)
+    for k in ("x", "vx", "vy", "life"):
+        assert_bitwise(got[k], want[k], k)
+    # y goes through logf (device ocml vs glibc): allow 1 ulp-level differences.
+    np.testing.assert_allclose(got["y"], want["y"], rtol=0, atol=1e-3)
+    assert (got["y"] >= cfg.screen_bounds[2]).all() and (got["y"] <= cfg.screen_bounds[3]).all()
+
+
+def test_full_size_sampled_parity(gpu, orc):
+    """BASELINE C3 size (1e8 particles): every particle is independent, so chunks sampled
+    across the whole array checked against the oracle with their global ids pin the full
+    launch (grid-stride coverage, 64-bit indexing, Philox counters at large ids)."""
+    rps = gpu
+    n = 100_000_000
+    cfg = config_c1(rps, n)
+    ext = rps.headline_ext()
+    g = np.random.default_rng(5)
+    chunk = 1 << 15
+    starts = sorted(set([0, n - chunk] + list(g.integers(0, n - chunk, 10))))
+    with rps.Context(n) as ctx:
+        ctx.set_config(cfg, ext)
+        ctx.init_scatter(seed=0x5EED)
+        ctx.step(4)  # gated frames
+        ctx.step(30)
+        fields = (rps.FIELD_X, rps.FIELD_Y, rps.FIELD_VX, rps.FIELD_VY, rps.FIELD_LIFE)
+        before = [{k: ctx.download_field(f, s, chunk) for k, f in zip(KEYS5, fields)} for s in starts]
+        ctx.step(3)
+        _, act = ctx.counters()
+        after = [{k: ctx.download_field(f, s, chunk) for k, f in zip(KEYS5, fields)} for s in starts]
+    assert act == 33
+    for s, b, a in zip(starts, before, after):
+        for k in range(30, 33):
+            orc.stream_step(cfg, ext, b, k, id_offset=s)
+        assert_soa_bitwise(a, b, keys=KEYS5, what=f"chunk@{s} ")
+
+
+def test_aos_roundtrip_and_errors(gpu):
+    rps = gpu
+    n = 5000
+    cfg = config_c1(rps, n)
+    parts = rps.setup_particles_scatter(cfg, n, seed=3)
+    parts["velocity"] = np.random.default_rng(2).normal(0, 50, (n, 2)).astype(F)
+    with rps.Context(n) as ctx:
+        ctx.set_config(cfg, rps.make_ext())
+        ctx.upload(parts)
+        got = ctx.download()
+        assert_bitwise(got["position"].reshape(-1), parts["position"].reshape(-1))
+        assert_bitwise(got["velocity"].reshape(-1), parts["velocity"].reshape(-1))
+        sub = ctx.download(offset=100, n=50)
+        assert_bitwise(sub["position"].reshape(-1), parts["position"][100:150].reshape(-1))
+        with pytest.raises(rps.RpsError) as e:
+            ctx.download(offset=n - 1, n=2)
+        assert e.value.status == rps.RPS_ERR_INVALID_ARGUMENT
+        bad = rps.make_ext()
+        bad.num_attractors = 9
+        with pytest.raises(rps.RpsError):
+            ctx.set_config(cfg, bad)
+        with pytest.raises(rps.RpsError) as e:
+            ctx.read_debug(rps.DEBUG_DENSITIES)
+        assert e.value.status == rps.RPS_ERR_UNSUPPORTED
+        with pytest.raises(rps.RpsError) as e:
+            ctx.stats()
+        assert e.value.status == rps.RPS_ERR_UNSUPPORTED
+    with pytest.raises(rps.RpsError):
+        rps.Context(0)
+
+
+def test_profiling_counts_dominant_kernel(gpu):
+    rps = gpu
+    n = 1 << 20
+    cfg = config_c1(rps, n)
+    with rps.Context(n) as ctx:
+        ctx.set_config(cfg, rps.headline_ext())
+        ctx.init_scatter()
+        ctx.step(5)
+        ctx.set_profiling(True)
+        ctx.step(7)
+        ms, cnt = ctx.kernel_time()
+        assert cnt == 7 and ms > 0
+        amt, unit = ctx.step_cost()
+        assert unit == "bytes" and amt == 40.0 * n
+        assert ctx.time_steps(3) > 0

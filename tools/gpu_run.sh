@@ -1,0 +1,45 @@
+#!/bin/bash
+# GPU-box driver for gpurun: runs the requested steps in order, each under its own time
+# limit, logs under gpurun_out/.  A test *failure* (pytest rc 1) lets later steps run; any
+# crash/abort/timeout (rc >= 2 from pytest, or != 0 from other steps) stops the script.
+#   tools/gpu_run.sh tests smoke bench prof
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+run() {
+  local name=$1 t=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -n 25 "gpurun_out/$name.log"
+  return $rc
+}
+for step in "$@"; do
+  case "$step" in
+    tests)
+      run pytest_gpu 900 python -m pytest tests -m gpu -q -rf --durations=15; rc=$?
+      [ $rc -le 1 ] || exit $rc ;;
+    smoke)
+      run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
+    bench)
+      run bench 600 python bench.py || exit $? ;;
+    bench_short)
+      run bench_short 300 python bench.py --steps 50 --warmup 10 --no-cpu-baseline || exit $? ;;
+    torchrun1)
+      run torchrun1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 1 --steps 50 --warmup 10 --no-cpu-baseline || exit $? ;;
+    prof)
+      run prof_trace 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace -o run --output-format csv -- python3 bench.py --steps 100 --warmup 10 --no-cpu-baseline || exit $? ;;
+    pmc)
+      run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline || exit $?
+      run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline || exit $? ;;
+    *)
+      # arbitrary python script under tools/: "py:tools/foo.py"
+      if [[ "$step" == py:* ]]; then
+        run "$(basename "${step#py:}" .py)" 900 python "${step#py:}" || exit $?
+      else
+        echo "unknown step $step"; exit 2
+      fi ;;
+  esac
+done
