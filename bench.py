@@ -37,6 +37,8 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=1 << 22, help="CPU-baseline particles")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=0x5EED)
+    ap.add_argument("--profile-every", type=int, default=8,
+                    help="bracket every k-th kernel launch with HIP events (roofline.achieved)")
     return ap.parse_args()
 
 
@@ -138,7 +140,7 @@ def main():
 
     d.sync_device()
     d.barrier()
-    ctx.set_profiling(True)
+    ctx.set_profiling(args.profile_every)
     t0 = time.perf_counter()
     ctx.step(args.steps)
     ctx.sync()

@@ -230,10 +230,12 @@ int rps_get_stats(rps_ctx* ctx, rps_stats* out);
 /* Host-visible counters: frame_count of the device config and active steps executed. */
 int rps_get_counters(const rps_ctx* ctx, uint32_t* frame_count, uint64_t* active_steps);
 
-/* Per-launch kernel timing with HIP events on the context stream (for bench.py). */
-int rps_set_profiling(rps_ctx* ctx, int enable);
-/* Average duration (ms) and count of the dominant kernel's launches since profiling was
- * enabled; blocks until they completed. */
+/* Per-launch kernel timing with HIP events on the context stream (for bench.py):
+ * period 0 = off, k > 0 = bracket every k-th launch of the mode's dominant kernel (stream
+ * step / N-body force / SPH simulation pass) with an event pair. */
+int rps_set_profiling(rps_ctx* ctx, int period);
+/* Average duration (ms) and count of the bracketed dominant-kernel launches since profiling
+ * was enabled; blocks until they completed. */
 int rps_get_kernel_time(rps_ctx* ctx, double* avg_ms, uint64_t* launches);
 /* Time nsteps rps_step calls with a pair of HIP events on the context stream. */
 int rps_time_steps(rps_ctx* ctx, uint32_t nsteps, double* total_ms);

@@ -35,6 +35,8 @@ struct rps_ctx {
 
   char* arena = nullptr;
   size_t arena_bytes = 0;
+  Layout layout = plain_layout();  // tiled for STREAM (rps_device.hpp)
+  float* state = nullptr;          // STREAM: the tiled x|y|vx|vy|life block
   float *x = nullptr, *y = nullptr, *vx = nullptr, *vy = nullptr, *life = nullptr;
   // SPH
   float *vx2 = nullptr, *vy2 = nullptr;
@@ -64,7 +66,9 @@ struct rps_ctx {
   uint64_t active_steps = 0;
   bool stepped = false;
   // profiling
-  bool profiling = false;
+  uint32_t profile_every = 0;  // 0: off; k: events around every k-th dominant launch
+  uint64_t profile_seq = 0;
+  bool profile_open = false;
   std::vector<hipEvent_t> ev_start, ev_stop;
   size_t ev_used = 0;
   // tuning
@@ -131,6 +135,10 @@ int check_ctx(rps_ctx* ctx) {
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return fail(ctx, RPS_ERR_DEVICE, std::string("hipSetDevice: ") + hipGetErrorString(e));
   return RPS_OK;
+}
+
+Fields fields(const rps_ctx* ctx) {
+  return Fields{ctx->x, ctx->y, ctx->vx, ctx->vy, ctx->life};
 }
 
 float* field_ptr(rps_ctx* ctx, int field) {
@@ -205,7 +213,8 @@ StreamArgs make_stream_args(const rps_ctx* ctx, uint64_t k) {
 }
 
 int prof_begin(rps_ctx* ctx) {
-  if (!ctx->profiling) return RPS_OK;
+  ctx->profile_open = ctx->profile_every && (ctx->profile_seq++ % ctx->profile_every == 0);
+  if (!ctx->profile_open) return RPS_OK;
   if (ctx->ev_used == ctx->ev_start.size()) {
     hipEvent_t a, b;
     RPS_HIP(ctx, hipEventCreate(&a));
@@ -218,7 +227,8 @@ int prof_begin(rps_ctx* ctx) {
 }
 
 int prof_end(rps_ctx* ctx) {
-  if (!ctx->profiling) return RPS_OK;
+  if (!ctx->profile_open) return RPS_OK;
+  ctx->profile_open = false;
   RPS_HIP(ctx, hipEventRecord(ctx->ev_stop[ctx->ev_used], ctx->stream));
   ++ctx->ev_used;
   return RPS_OK;
@@ -257,7 +267,7 @@ int step_stream(rps_ctx* ctx) {
   if (stats && l.grid > ctx->partial_cap) {
     if (ctx->partials) RPS_HIP(ctx, hipFree(ctx->partials));
     ctx->partials = nullptr;
-    RPS_HIP(ctx, hipMalloc(&ctx->partials, sizeof(StatsPartial) * l.grid));
+    RPS_HIP(ctx, hipMalloc(&ctx->partials, sizeof(StatsPartial) * (l.grid + kStatsFold)));
     ctx->partial_cap = l.grid;
     a.partials = ctx->partials;
   }
@@ -267,7 +277,8 @@ int step_stream(rps_ctx* ctx) {
   rc = prof_end(ctx);
   if (rc) return rc;
   if (stats) {
-    RPS_HIP(ctx, launch_stats_finalize(ctx->partials, l.grid, ctx->d_stats, k, ctx->stream));
+    RPS_HIP(ctx, launch_stats_finalize(ctx->partials, l.grid, ctx->partials + ctx->partial_cap,
+                                       ctx->d_stats, k, ctx->stream));
     ctx->have_stats = true;
   }
   return RPS_OK;
@@ -419,11 +430,16 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
   size_t off = 0;
   struct Slot { void** p; size_t bytes; };
   std::vector<Slot> slots;
-  slots.push_back({(void**)&ctx->x, nf});
-  slots.push_back({(void**)&ctx->y, nf});
-  slots.push_back({(void**)&ctx->vx, nf});
-  slots.push_back({(void**)&ctx->vy, nf});
-  if (ctx->mode == RPS_MODE_STREAM) slots.push_back({(void**)&ctx->life, nf});
+  if (ctx->mode == RPS_MODE_STREAM) {
+    // Tiled SoA: ceil(n / kTile) tiles of kFields x kTile floats (rps_device.hpp).
+    const size_t tiles = (n + kTile - 1) / kTile;
+    slots.push_back({(void**)&ctx->state, tiles * kFields * kTile * sizeof(float)});
+  } else {
+    slots.push_back({(void**)&ctx->x, nf});
+    slots.push_back({(void**)&ctx->y, nf});
+    slots.push_back({(void**)&ctx->vx, nf});
+    slots.push_back({(void**)&ctx->vy, nf});
+  }
   if (ctx->mode == RPS_MODE_SPH) {
     ctx->P = next_pow2_u32((uint32_t)n);  // spatial lookup sized next_pow2 (particle_buffers.rs:86)
     slots.push_back({(void**)&ctx->vx2, nf});
@@ -453,6 +469,14 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     return bail(e == hipErrorOutOfMemory ? RPS_ERR_OUT_OF_MEMORY : RPS_ERR_DEVICE);
   }
   for (size_t i = 0; i < slots.size(); ++i) *slots[i].p = ctx->arena + offs[i];
+  if (ctx->mode == RPS_MODE_STREAM) {
+    ctx->layout = tiled_layout();
+    ctx->x = ctx->state;
+    ctx->y = ctx->state + kTile;
+    ctx->vx = ctx->state + 2 * kTile;
+    ctx->vy = ctx->state + 3 * kTile;
+    ctx->life = ctx->state + 4 * kTile;
+  }
   // wgpu buffers are zero-initialised; the SPH lookup pad entries rely on it.
   if (hipMemsetAsync(ctx->arena, 0, ctx->arena_bytes, ctx->stream) != hipSuccess) {
     ctx->err = "hipMemsetAsync failed";
@@ -545,8 +569,7 @@ int rps_upload_particles(rps_ctx* ctx, const rps_particle* aos, uint64_t offset,
     RPS_HIP(ctx, hipMemcpyAsync(ctx->d_staging, aos + done, m * sizeof(rps_particle),
                                 hipMemcpyHostToDevice, ctx->stream));
     const uint64_t o = offset + done;
-    RPS_HIP(ctx, launch_aos_to_soa(ctx->d_staging, ctx->x + o, ctx->y + o, ctx->vx + o,
-                                   ctx->vy + o, m, ctx->stream));
+    RPS_HIP(ctx, launch_aos_to_soa(ctx->d_staging, fields(ctx), ctx->layout, o, m, ctx->stream));
     RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
   }
   return RPS_OK;
@@ -564,8 +587,8 @@ int rps_download_particles(rps_ctx* ctx, rps_particle* aos, uint64_t offset, uin
   for (uint64_t done = 0; done < n; done += chunk) {
     const uint64_t m = std::min(chunk, n - done);
     const uint64_t o = offset + done;
-    RPS_HIP(ctx, launch_soa_to_aos(ctx->x + o, ctx->y + o, ctx->vx + o, ctx->vy + o, ctx->d_staging,
-                                   m, ctx->cfg.max_energy, ctx->stepped ? 0 : 1, ctx->stream));
+    RPS_HIP(ctx, launch_soa_to_aos(fields(ctx), ctx->layout, o, ctx->d_staging, m,
+                                   ctx->cfg.max_energy, ctx->stepped ? 0 : 1, ctx->stream));
     RPS_HIP(ctx, hipMemcpyAsync(aos + done, ctx->d_staging, m * sizeof(rps_particle),
                                 hipMemcpyDeviceToHost, ctx->stream));
     RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -581,8 +604,22 @@ int rps_upload_field(rps_ctx* ctx, int field, const float* src, uint64_t offset,
   if (!src && n) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "null source");
   if (offset + n > ctx->n) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "range exceeds particle_count");
   if (n == 0) return RPS_OK;
-  RPS_HIP(ctx, hipMemcpyAsync(p + offset, src, n * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
-  RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (ctx->layout.mask == plain_layout().mask) {
+    RPS_HIP(ctx, hipMemcpyAsync(p + offset, src, n * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+    RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return RPS_OK;
+  }
+  // Tiled layout: dense chunk -> staging -> scatter into the tiles.
+  const uint64_t chunk = std::min<uint64_t>(n, kStagingChunk * (sizeof(rps_particle) / sizeof(float)));
+  rc = ensure_staging(ctx, (chunk * sizeof(float) + sizeof(rps_particle) - 1) / sizeof(rps_particle));
+  if (rc) return rc;
+  float* stage = reinterpret_cast<float*>(ctx->d_staging);
+  for (uint64_t done = 0; done < n; done += chunk) {
+    const uint64_t m = std::min(chunk, n - done);
+    RPS_HIP(ctx, hipMemcpyAsync(stage, src + done, m * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+    RPS_HIP(ctx, launch_field_scatter(p, ctx->layout, offset + done, stage, m, ctx->stream));
+    RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  }
   return RPS_OK;
 }
 
@@ -594,8 +631,21 @@ int rps_download_field(rps_ctx* ctx, int field, float* dst, uint64_t offset, uin
   if (!dst && n) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "null destination");
   if (offset + n > ctx->n) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "range exceeds particle_count");
   if (n == 0) return RPS_OK;
-  RPS_HIP(ctx, hipMemcpyAsync(dst, p + offset, n * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
-  RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (ctx->layout.mask == plain_layout().mask) {
+    RPS_HIP(ctx, hipMemcpyAsync(dst, p + offset, n * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+    RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return RPS_OK;
+  }
+  const uint64_t chunk = std::min<uint64_t>(n, kStagingChunk * (sizeof(rps_particle) / sizeof(float)));
+  rc = ensure_staging(ctx, (chunk * sizeof(float) + sizeof(rps_particle) - 1) / sizeof(rps_particle));
+  if (rc) return rc;
+  float* stage = reinterpret_cast<float*>(ctx->d_staging);
+  for (uint64_t done = 0; done < n; done += chunk) {
+    const uint64_t m = std::min(chunk, n - done);
+    RPS_HIP(ctx, launch_field_gather(p, ctx->layout, offset + done, stage, m, ctx->stream));
+    RPS_HIP(ctx, hipMemcpyAsync(dst + done, stage, m * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+    RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  }
   return RPS_OK;
 }
 
@@ -627,11 +677,8 @@ int rps_init_scatter(rps_ctx* ctx, uint64_t seed) {
   if (rc) return rc;
   if (!ctx->have_config) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "rps_set_config first");
   InitArgs a;
-  a.x = ctx->x;
-  a.y = ctx->y;
-  a.vx = ctx->vx;
-  a.vy = ctx->vy;
-  a.life = (ctx->mode == RPS_MODE_STREAM) ? ctx->life : nullptr;
+  a.f = fields(ctx);
+  a.layout = ctx->layout;
   a.n = ctx->n;
   a.id_offset = ctx->id_offset;
   a.x_min = ctx->cfg.screen_bounds[0];
@@ -710,7 +757,9 @@ int rps_get_counters(const rps_ctx* ctx, uint32_t* frame_count, uint64_t* active
 int rps_set_profiling(rps_ctx* ctx, int enable) {
   int rc = check_ctx(ctx);
   if (rc) return rc;
-  ctx->profiling = enable != 0;
+  if (enable < 0) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "profiling period must be >= 0");
+  ctx->profile_every = (uint32_t)enable;
+  ctx->profile_seq = 0;
   ctx->ev_used = 0;
   return RPS_OK;
 }

@@ -22,21 +22,24 @@ struct StreamLaunch {
 uint32_t stream_blocks_for(uint64_t n);
 
 hipError_t launch_stream_step(const StreamArgs& a, const StreamLaunch& l, hipStream_t s);
+// Deterministic two-level reduction of per-workgroup partials (scratch: kStatsFold entries).
+constexpr uint32_t kStatsFold = 256;
 hipError_t launch_stats_finalize(const StatsPartial* partials, uint32_t count,
-                                 StatsResult* out, uint64_t step, hipStream_t s);
+                                 StatsPartial* scratch, StatsResult* out, uint64_t step,
+                                 hipStream_t s);
 
-hipError_t launch_aos_to_soa(const rps_particle* aos, float* x, float* y, float* vx, float* vy,
+hipError_t launch_aos_to_soa(const rps_particle* aos, Fields f, Layout L, uint64_t offset,
                              uint64_t n, hipStream_t s);
-hipError_t launch_soa_to_aos(const float* x, const float* y, const float* vx, const float* vy,
-                             rps_particle* aos, uint64_t n, float max_energy, int spawn_colour,
-                             hipStream_t s);
+hipError_t launch_soa_to_aos(Fields f, Layout L, uint64_t offset, rps_particle* aos, uint64_t n,
+                             float max_energy, int spawn_colour, hipStream_t s);
+hipError_t launch_field_gather(const float* field, Layout L, uint64_t offset, float* out,
+                               uint64_t n, hipStream_t s);
+hipError_t launch_field_scatter(float* field, Layout L, uint64_t offset, const float* in,
+                                uint64_t n, hipStream_t s);
 
 struct InitArgs {
-  float* x;
-  float* y;
-  float* vx;
-  float* vy;
-  float* life;  // may be null
+  Fields f;  // life may be null
+  Layout layout;
   uint64_t n, id_offset;
   float x_min, x_max, y_min, y_max, global_count_f, life_min, life_range;
   uint32_t key0, key1;

@@ -109,12 +109,13 @@ __global__ __launch_bounds__(kBlock) void stream_step_kernel(StreamArgs a) {
   if constexpr (STATS) acc.init();
   for (uint64_t v = tid; v < nvec; v += stride) {
     const uint64_t i = v << 2;
-    f4 X = ld4<NT>(a.x + i);
-    f4 Y = ld4<NT>(a.y + i);
-    f4 VX = ld4<NT>(a.vx + i);
-    f4 VY = ld4<NT>(a.vy + i);
+    const uint64_t o = tidx(i);  // 4 consecutive particles never straddle a tile
+    f4 X = ld4<NT>(a.x + o);
+    f4 Y = ld4<NT>(a.y + o);
+    f4 VX = ld4<NT>(a.vx + o);
+    f4 VY = ld4<NT>(a.vy + o);
     f4 L = {0.0f, 0.0f, 0.0f, 0.0f};
-    if constexpr (LIFETIME) L = ld4<NT>(a.life + i);
+    if constexpr (LIFETIME) L = ld4<NT>(a.life + o);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       float x = X[c], y = Y[c], vx = VX[c], vy = VY[c], life = L[c];
@@ -126,27 +127,50 @@ __global__ __launch_bounds__(kBlock) void stream_step_kernel(StreamArgs a) {
       L[c] = life;
       if constexpr (STATS) acc.add(x, y, vx, vy, re);
     }
-    st4<NT>(a.x + i, X);
-    st4<NT>(a.y + i, Y);
-    st4<NT>(a.vx + i, VX);
-    st4<NT>(a.vy + i, VY);
-    if constexpr (LIFETIME) st4<NT>(a.life + i, L);
+    st4<NT>(a.x + o, X);
+    st4<NT>(a.y + o, Y);
+    st4<NT>(a.vx + o, VX);
+    st4<NT>(a.vy + o, VY);
+    if constexpr (LIFETIME) st4<NT>(a.life + o, L);
   }
   // n % 4 tail particles, one per lane of the first threads.
   const uint64_t rem = a.n - (nvec << 2);
   if (tid < rem) {
     const uint64_t i = (nvec << 2) + tid;
-    float x = a.x[i], y = a.y[i], vx = a.vx[i], vy = a.vy[i];
-    float life = LIFETIME ? a.life[i] : 0.0f;
+    const uint64_t o = tidx(i);
+    float x = a.x[o], y = a.y[o], vx = a.vx[o], vy = a.vy[o];
+    float life = LIFETIME ? a.life[o] : 0.0f;
     const bool re = step_one<VERLET, LIFETIME>(a, a.id_offset + i, x, y, vx, vy, life);
-    a.x[i] = x;
-    a.y[i] = y;
-    a.vx[i] = vx;
-    a.vy[i] = vy;
-    if constexpr (LIFETIME) a.life[i] = life;
+    a.x[o] = x;
+    a.y[o] = y;
+    a.vx[o] = vx;
+    a.vy[o] = vy;
+    if constexpr (LIFETIME) a.life[o] = life;
     if constexpr (STATS) acc.add(x, y, vx, vy, re);
   }
   if constexpr (STATS) block_reduce_stats(acc, a.partials);
+}
+
+// First level of the fixed-order partial reduction: workgroup b folds partials
+// [b*chunk, (b+1)*chunk) so the single-workgroup finalize reads at most 256 entries.
+__global__ __launch_bounds__(kBlock) void stats_fold_kernel(const StatsPartial* partials,
+                                                            uint32_t count, uint32_t chunk,
+                                                            StatsPartial* out) {
+  StatsAcc acc;
+  acc.init();
+  const uint32_t lo = blockIdx.x * chunk;
+  const uint32_t hi = min(count, lo + chunk);
+  for (uint32_t i = lo + threadIdx.x; i < hi; i += kBlock) {
+    const StatsPartial p = partials[i];
+    acc.x0 = fminf(acc.x0, p.bbox[0]);
+    acc.x1 = fmaxf(acc.x1, p.bbox[1]);
+    acc.y0 = fminf(acc.y0, p.bbox[2]);
+    acc.y1 = fmaxf(acc.y1, p.bbox[3]);
+    acc.ke += p.ke;
+    acc.count += p.count;
+    acc.respawned += p.respawned;
+  }
+  block_reduce_stats(acc, out);
 }
 
 __global__ __launch_bounds__(kBlock) void stats_finalize_kernel(const StatsPartial* partials,
@@ -181,28 +205,43 @@ __global__ __launch_bounds__(kBlock) void stats_finalize_kernel(const StatsParti
 // ---------------------------------------------------------------------------------------
 // AoS <-> SoA (the 32-B Particle of src/particle.rs:20-25)
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void aos_to_soa_kernel(const rps_particle* aos, float* x,
-                                                            float* y, float* vx, float* vy,
-                                                            uint64_t n) {
-  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  const f4 pv = *reinterpret_cast<const f4*>(&aos[i].position[0]);
-  x[i] = pv[0];
-  y[i] = pv[1];
-  vx[i] = pv[2];
-  vy[i] = pv[3];
+__global__ __launch_bounds__(kBlock) void aos_to_soa_kernel(const rps_particle* aos, Fields f,
+                                                            Layout L, uint64_t offset, uint64_t n) {
+  const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j >= n) return;
+  const f4 pv = *reinterpret_cast<const f4*>(&aos[j].position[0]);
+  const uint64_t o = lidx(L, offset + j);
+  f.x[o] = pv[0];
+  f.y[o] = pv[1];
+  f.vx[o] = pv[2];
+  f.vy[o] = pv[3];
 }
 
-__global__ __launch_bounds__(kBlock) void soa_to_aos_kernel(const float* x, const float* y,
-                                                            const float* vx, const float* vy,
+__global__ __launch_bounds__(kBlock) void soa_to_aos_kernel(Fields f, Layout L, uint64_t offset,
                                                             rps_particle* aos, uint64_t n,
                                                             float max_energy, int spawn_colour) {
-  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  const float qx = vx[i], qy = vy[i];
-  *reinterpret_cast<f4*>(&aos[i].position[0]) = f4{x[i], y[i], qx, qy};
+  const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j >= n) return;
+  const uint64_t o = lidx(L, offset + j);
+  const float qx = f.vx[o], qy = f.vy[o];
+  *reinterpret_cast<f4*>(&aos[j].position[0]) = f4{f.x[o], f.y[o], qx, qy};
   const f4 c = spawn_colour ? f4{1.0f, 1.0f, 1.0f, 1.0f} : set_color(qx, qy, max_energy);
-  *reinterpret_cast<f4*>(&aos[i].color[0]) = c;
+  *reinterpret_cast<f4*>(&aos[j].color[0]) = c;
+}
+
+// One field <-> a dense float range (checkpoint / SoA transfers through the layout).
+__global__ __launch_bounds__(kBlock) void field_gather_kernel(const float* field, Layout L,
+                                                              uint64_t offset, float* out,
+                                                              uint64_t n) {
+  const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j < n) out[j] = field[lidx(L, offset + j)];
+}
+
+__global__ __launch_bounds__(kBlock) void field_scatter_kernel(float* field, Layout L,
+                                                               uint64_t offset, const float* in,
+                                                               uint64_t n) {
+  const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j < n) field[lidx(L, offset + j)] = in[j];
 }
 
 // ---------------------------------------------------------------------------------------
@@ -212,8 +251,9 @@ __global__ __launch_bounds__(kBlock) void init_scatter_kernel(InitArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= a.n) return;
   const uint64_t g = a.id_offset + i;
+  const uint64_t o = lidx(a.layout, i);
   const float t = (float)g / a.global_count_f;
-  a.x[i] = a.x_min + t * (a.x_max - a.x_min);
+  a.f.x[o] = a.x_min + t * (a.x_max - a.x_min);
   uint32_t w[4];
   philox4x32_10((uint32_t)g, (uint32_t)(g >> 32), 0xFFFFFFFFu, 0xFFFFFFFFu, a.key0, a.key1, w);
   const float u1 = (float)((w[0] >> 8) + 1u) * (1.0f / 16777216.0f);
@@ -225,10 +265,10 @@ __global__ __launch_bounds__(kBlock) void init_scatter_kernel(InitArgs a) {
   float yy = y_center + z * y_sd;
   yy = yy < a.y_min ? a.y_min : yy;
   yy = yy > a.y_max ? a.y_max : yy;
-  a.y[i] = yy;
-  a.vx[i] = 0.0f;
-  a.vy[i] = 0.0f;
-  if (a.life) a.life[i] = a.life_min + u01(w[2]) * a.life_range;
+  a.f.y[o] = yy;
+  a.f.vx[o] = 0.0f;
+  a.f.vy[o] = 0.0f;
+  if (a.f.life) a.f.life[o] = a.life_min + u01(w[2]) * a.life_range;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -619,27 +659,52 @@ hipError_t launch_stream_step(const StreamArgs& a, const StreamLaunch& l, hipStr
   }
 }
 
-hipError_t launch_stats_finalize(const StatsPartial* partials, uint32_t count, StatsResult* out,
-                                 uint64_t step, hipStream_t s) {
+hipError_t launch_stats_finalize(const StatsPartial* partials, uint32_t count,
+                                 StatsPartial* scratch, StatsResult* out, uint64_t step,
+                                 hipStream_t s) {
+  if (count > kStatsFold) {
+    const uint32_t chunk = (count + kStatsFold - 1) / kStatsFold;
+    const uint32_t blocks = (count + chunk - 1) / chunk;
+    hipLaunchKernelGGL(stats_fold_kernel, dim3(blocks), dim3(kBlock), 0, s, partials, count, chunk,
+                       scratch);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    partials = scratch;
+    count = blocks;
+  }
   hipLaunchKernelGGL(stats_finalize_kernel, dim3(1), dim3(kBlock), 0, s, partials, count, out,
                      (unsigned long long)step);
   return hipGetLastError();
 }
 
-hipError_t launch_aos_to_soa(const rps_particle* aos, float* x, float* y, float* vx, float* vy,
+hipError_t launch_aos_to_soa(const rps_particle* aos, Fields f, Layout L, uint64_t offset,
                              uint64_t n, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(aos_to_soa_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, s, aos, x, y, vx,
-                     vy, n);
+  hipLaunchKernelGGL(aos_to_soa_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, s, aos, f, L, offset, n);
   return hipGetLastError();
 }
 
-hipError_t launch_soa_to_aos(const float* x, const float* y, const float* vx, const float* vy,
-                             rps_particle* aos, uint64_t n, float max_energy, int spawn_colour,
-                             hipStream_t s) {
+hipError_t launch_soa_to_aos(Fields f, Layout L, uint64_t offset, rps_particle* aos, uint64_t n,
+                             float max_energy, int spawn_colour, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(soa_to_aos_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, s, x, y, vx, vy,
-                     aos, n, max_energy, spawn_colour);
+  hipLaunchKernelGGL(soa_to_aos_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, s, f, L, offset, aos,
+                     n, max_energy, spawn_colour);
+  return hipGetLastError();
+}
+
+hipError_t launch_field_gather(const float* field, Layout L, uint64_t offset, float* out,
+                               uint64_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(field_gather_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, s, field, L, offset,
+                     out, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_field_scatter(float* field, Layout L, uint64_t offset, const float* in,
+                                uint64_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(field_scatter_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, s, field, L,
+                     offset, in, n);
   return hipGetLastError();
 }
 

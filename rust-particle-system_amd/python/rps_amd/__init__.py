@@ -482,8 +482,9 @@ class Context:
         self._call("rps_get_counters", ctypes.byref(fc), ctypes.byref(act))
         return fc.value, act.value
 
-    def set_profiling(self, on: bool):
-        self._call("rps_set_profiling", 1 if on else 0)
+    def set_profiling(self, period=1):
+        """0/False: off; k: HIP-event pair around every k-th dominant-kernel launch."""
+        self._call("rps_set_profiling", int(period))
 
     def kernel_time(self):
         ms, cnt = ctypes.c_double(), ctypes.c_uint64()

@@ -34,6 +34,8 @@ for step in "$@"; do
     pmc)
       run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline || exit $?
       run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline || exit $? ;;
+    probe)
+      run hbm_probe 300 tools/hbm_probe || exit $? ;;
     *)
       # arbitrary python script under tools/: "py:tools/foo.py"
       if [[ "$step" == py:* ]]; then
