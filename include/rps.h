@@ -232,7 +232,8 @@ int rps_get_counters(const rps_ctx* ctx, uint32_t* frame_count, uint64_t* active
 
 /* Per-launch kernel timing with HIP events on the context stream (for bench.py):
  * period 0 = off, k > 0 = bracket every k-th launch of the mode's dominant kernel (stream
- * step / N-body force / SPH simulation pass) with an event pair. */
+ * step / N-body force / SPH simulation pass) with an event pair.  Stream steps that also
+ * fuse the stats reduction are a different kernel variant and are not sampled. */
 int rps_set_profiling(rps_ctx* ctx, int period);
 /* Average duration (ms) and count of the bracketed dominant-kernel launches since profiling
  * was enabled; blocks until they completed. */

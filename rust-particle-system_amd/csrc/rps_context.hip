@@ -212,8 +212,11 @@ StreamArgs make_stream_args(const rps_ctx* ctx, uint64_t k) {
   return a;
 }
 
-int prof_begin(rps_ctx* ctx) {
-  ctx->profile_open = ctx->profile_every && (ctx->profile_seq++ % ctx->profile_every == 0);
+// `sampled` = false for launches that are a different kernel variant than the dominant one
+// (the stats-fused stream step every stats_interval steps), so the average matches the
+// rocprofv3 per-kernel figure of the dominant kernel.
+int prof_begin(rps_ctx* ctx, bool sampled = true) {
+  ctx->profile_open = sampled && ctx->profile_every && (ctx->profile_seq++ % ctx->profile_every == 0);
   if (!ctx->profile_open) return RPS_OK;
   if (ctx->ev_used == ctx->ev_start.size()) {
     hipEvent_t a, b;
@@ -271,7 +274,7 @@ int step_stream(rps_ctx* ctx) {
     ctx->partial_cap = l.grid;
     a.partials = ctx->partials;
   }
-  int rc = prof_begin(ctx);
+  int rc = prof_begin(ctx, !stats);
   if (rc) return rc;
   RPS_HIP(ctx, launch_stream_step(a, l, ctx->stream));
   rc = prof_end(ctx);

@@ -30,10 +30,10 @@ for step in "$@"; do
     torchrun1)
       run torchrun1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 1 --steps 50 --warmup 10 --no-cpu-baseline || exit $? ;;
     prof)
-      run prof_trace 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace -o run --output-format csv -- python3 bench.py --steps 100 --warmup 10 --no-cpu-baseline || exit $? ;;
+      run prof_trace 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace -o run --output-format csv -- python3 bench.py --no-cpu-baseline || exit $? ;;
     pmc)
-      run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline || exit $?
-      run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline || exit $? ;;
+      run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 40 --warmup 10 --no-cpu-baseline || exit $?
+      run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 40 --warmup 10 --no-cpu-baseline || exit $? ;;
     probe)
       run hbm_probe 300 tools/hbm_probe || exit $? ;;
     *)
