@@ -551,18 +551,23 @@ def prepare_particle_buffers(system: ParticleSystem, config: ParticleConfig,
                              ext: Optional[ExtConfig] = None, device: int = 0) -> GPUPipelineBuffers:
     """prepare_particle_buffers, src/particle_buffers.rs:38-237.
 
-    First call: allocate buffers and upload the particles once (:50-216).  Later calls:
-    re-upload the config (:218-236).  The per-frame frame_count increment of :227 happens
-    inside ParticleComputeNode.run (rps_step), keeping the config's frame_count in sync.
+    First call: allocate buffers and upload the particles once (:50-216).  Later calls model
+    the render-world config copy: `config` is the main-world resource (frame_count never
+    incremented there; the render-world increment of :227 happens in rps_step).  Bevy
+    re-extracts it only when it changed (src/particle.rs:35), carrying frame_count = 0, so a
+    GUI change resets frame_count and re-arms SHADER_DELAY.
     """
     if buffers is None:
         ctx = Context(len(system.particles), mode=mode, device=device)
         ctx.set_config(config, ext)
         ctx.upload(system.particles)
         return GPUPipelineBuffers(ctx)
-    c, _ = buffers.ctx.get_config()
-    config.frame_count = c.frame_count
-    buffers.ctx.set_config(config, ext)
+    cur, cur_ext = buffers.ctx.get_config()
+    probe = ParticleConfig.from_buffer_copy(bytes(config))
+    probe.frame_count = cur.frame_count
+    changed = bytes(probe) != bytes(cur) or (ext is not None and bytes(ext) != bytes(cur_ext))
+    if changed:
+        buffers.ctx.set_config(config, ext)
     return buffers
 
 
