@@ -39,7 +39,8 @@ struct rps_ctx {
   float* state = nullptr;          // STREAM: the tiled x|y|vx|vy|life block
   float *x = nullptr, *y = nullptr, *vx = nullptr, *vy = nullptr, *life = nullptr;
   // SPH
-  float *vx2 = nullptr, *vy2 = nullptr;
+  float *vx2 = nullptr, *vy2 = nullptr, *x2 = nullptr, *y2 = nullptr;
+  f2 *pred_s = nullptr, *vel_s = nullptr, *dens_s = nullptr;
   uint2* lookup = nullptr;
   uint32_t* offsets = nullptr;
   f2* dens = nullptr;
@@ -246,6 +247,11 @@ SphBuffers sph_buffers(rps_ctx* ctx) {
   b.vy = ctx->vy;
   b.vx2 = ctx->vx2;
   b.vy2 = ctx->vy2;
+  b.x2 = ctx->x2;
+  b.y2 = ctx->y2;
+  b.pred_s = ctx->pred_s;
+  b.vel_s = ctx->vel_s;
+  b.dens_s = ctx->dens_s;
   b.lookup = ctx->lookup;
   b.offsets = ctx->offsets;
   b.dens = ctx->dens;
@@ -345,6 +351,8 @@ int step_sph_sim(rps_ctx* ctx) {
   if (rc) return rc;
   std::swap(ctx->vx, ctx->vx2);
   std::swap(ctx->vy, ctx->vy2);
+  std::swap(ctx->x, ctx->x2);
+  std::swap(ctx->y, ctx->y2);
   return RPS_OK;
 }
 
@@ -447,6 +455,11 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     ctx->P = next_pow2_u32((uint32_t)n);  // spatial lookup sized next_pow2 (particle_buffers.rs:86)
     slots.push_back({(void**)&ctx->vx2, nf});
     slots.push_back({(void**)&ctx->vy2, nf});
+    slots.push_back({(void**)&ctx->x2, nf});
+    slots.push_back({(void**)&ctx->y2, nf});
+    slots.push_back({(void**)&ctx->pred_s, align_up(n * sizeof(f2), 256)});
+    slots.push_back({(void**)&ctx->vel_s, align_up(n * sizeof(f2), 256)});
+    slots.push_back({(void**)&ctx->dens_s, align_up(n * sizeof(f2), 256)});
     slots.push_back({(void**)&ctx->lookup, align_up((size_t)ctx->P * sizeof(uint2), 256)});
     slots.push_back({(void**)&ctx->offsets, align_up(n * sizeof(uint32_t), 256)});
     slots.push_back({(void**)&ctx->dens, align_up(n * sizeof(f2), 256)});

@@ -75,10 +75,18 @@ struct SphBuffers {
   float* vy;
   float* vx2;   // sim-pass output velocities (swapped with vx/vy after the pass)
   float* vy2;
+  float* x2;    // sim-pass output positions (swapped with x/y after the pass)
+  float* y2;
   uint2* lookup;     // P entries
   uint32_t* offsets; // N
   f2* dens;          // N
   f2* pred;          // N
+  // Neighbour data gathered into spatial-lookup order (entry j holds particle lookup[j].y's
+  // value), so a cell's entries are contiguous: pred_s/vel_s after prediction, dens_s after
+  // the density pass.
+  f2* pred_s;        // N
+  f2* vel_s;         // N
+  f2* dens_s;        // N
   uint32_t n;        // N
   uint32_t p;        // next_pow2(N)
 };

@@ -407,7 +407,7 @@ __global__ __launch_bounds__(kBlock) void sph_sort_global_kernel(uint2* __restri
   }
 }
 
-constexpr uint32_t kSortTile = 2048;  // entries per workgroup tile (16 KiB of LDS)
+constexpr uint32_t kSortTile = 8192;  // entries per workgroup tile (64 KiB of LDS)
 
 // Every remaining pass of stages [stage_lo, stage_hi] whose group_width fits one tile:
 // a pass with 2*gw <= tile only pairs entries inside aligned blocks of 2*gw, so a tile of
@@ -471,14 +471,53 @@ __global__ __launch_bounds__(kBlock) void sph_predict_kernel(const rps_config* _
 __constant__ int32_t kGridOff[9][2] = {{-1, -1}, {-1, 0}, {-1, 1}, {0, -1}, {0, 0},
                                        {0, 1},   {1, -1}, {1, 0},  {1, 1}};
 
-// calculate_density, compute_shader.wgsl:207-254.
+// Neighbour data in lookup order: entry j <- particle lookup[j].y (wgsl:239-240, :313-314,
+// :371 read exactly these values, pads included).
+__global__ __launch_bounds__(kBlock) void sph_gather_pv_kernel(const uint2* __restrict__ lookup,
+                                                               const f2* __restrict__ pred,
+                                                               const float* __restrict__ vx,
+                                                               const float* __restrict__ vy,
+                                                               f2* __restrict__ pred_s,
+                                                               f2* __restrict__ vel_s, uint32_t n) {
+  const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
+  if (j >= n) return;
+  const uint32_t i = lookup[j].y;
+  pred_s[j] = pred[i];
+  vel_s[j] = f2{vx[i], vy[i]};
+}
+
+__global__ __launch_bounds__(kBlock) void sph_gather_dens_kernel(const uint2* __restrict__ lookup,
+                                                                 const f2* __restrict__ dens,
+                                                                 f2* __restrict__ dens_s,
+                                                                 uint32_t n) {
+  const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
+  if (j >= n) return;
+  dens_s[j] = dens[lookup[j].y];
+}
+
+constexpr int kScanBatch = 4;  // lookup entries in flight per lane in the neighbour scans
+
+__device__ __forceinline__ uint32_t grid_key(int32_t cx, int32_t cy, int o, uint32_t N) {
+  return cell_key((int32_t)((uint32_t)cx + (uint32_t)kGridOff[o][0]),
+                  (int32_t)((uint32_t)cy + (uint32_t)kGridOff[o][1]), N);
+}
+
+// Work mapping of the density and sim passes: thread t takes the particle in lookup slot t,
+// t in [0, P).  Lanes of a wave then hold spatially adjacent particles and scan the same
+// cells.  Every particle's fresh entry is in exactly one slot; pad slots
+// repeat some particle, whose recomputation writes the identical value (all outputs are
+// separate buffers), so the race is benign and results are independent of it.
+//
+// calculate_density, compute_shader.wgsl:207-254, entries summed in lookup order.
 __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* __restrict__ cfg,
                                                              const uint2* __restrict__ lookup,
                                                              const uint32_t* __restrict__ offsets,
                                                              const f2* __restrict__ pred,
-                                                             f2* __restrict__ dens, uint32_t n) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
+                                                             const f2* __restrict__ pred_s,
+                                                             f2* __restrict__ dens, uint32_t p_slots) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= p_slots) return;
+  const uint32_t i = lookup[t].y;
   const float r = cfg->smoothing_radius, r2 = r * r;
   const uint32_t N = cfg->particle_count;
   const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
@@ -487,45 +526,67 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
   const int32_t cy = f32_to_i32((p[1] + cfg->screen_bounds[3]) / r);
   float d = 0.0f, nd = 0.0f;
   for (int o = 0; o < 9; ++o) {
-    const uint32_t key = cell_key((int32_t)((uint32_t)cx + (uint32_t)kGridOff[o][0]),
-                                  (int32_t)((uint32_t)cy + (uint32_t)kGridOff[o][1]), N);
-    for (uint32_t j = offsets[key]; j < N; ++j) {
-      const uint2 e = lookup[j];
-      if (e.x != key) break;
-      const f2 q = pred[e.y];
-      const float dx = p[0] - q[0], dy = p[1] - q[1];
-      const float sq = dx * dx + dy * dy;
-      if (sq > r2) continue;
-      const float dist = sqrtf(sq);
-      float k1 = 0.0f, k2 = 0.0f;
-      if (!(dist >= r)) {
-        const float v = r - dist;
-        k1 = (dn * v) * v;
-        k2 = ((ndn * v) * v) * v;
+    const uint32_t key = grid_key(cx, cy, o, N);
+    for (uint32_t j = offsets[key]; j < N; j += kScanBatch) {
+      uint32_t k[kScanBatch];
+      f2 q[kScanBatch];
+#pragma unroll
+      for (int u = 0; u < kScanBatch; ++u) {
+        const uint32_t jj = min(j + u, N - 1u);
+        k[u] = lookup[jj].x;
+        q[u] = pred_s[jj];
       }
-      d = d + k1;
-      nd = nd + k2;
+      bool stop = false;
+#pragma unroll
+      for (int u = 0; u < kScanBatch; ++u) {
+        if (!stop) {
+          if (j + u >= N || k[u] != key) {
+            stop = true;
+          } else {
+            const float dx = p[0] - q[u][0], dy = p[1] - q[u][1];
+            const float sq = dx * dx + dy * dy;
+            if (!(sq > r2)) {
+              const float dist = sqrtf(sq);
+              float k1 = 0.0f, k2 = 0.0f;
+              if (!(dist >= r)) {
+                const float v = r - dist;
+                k1 = (dn * v) * v;
+                k2 = ((ndn * v) * v) * v;
+              }
+              d = d + k1;
+              nd = nd + k2;
+            }
+          }
+        }
+      }
+      if (stop) break;
     }
   }
   dens[i] = f2{d, nd};
 }
 
 // simulation_step, compute_shader.wgsl:435-453: pressure (:256-334) and viscosity
-// (:336-384) against the start-of-pass velocity snapshot (vx, vy), Euler (:392-395) and
-// walls (:69-99).  New velocities go to (vx2, vy2); positions update in place.
+// (:336-384) against the start-of-pass velocity snapshot (vel_s), Euler (:392-395) and walls
+// (:69-99).  New velocities/positions go to (vx2, vy2, x2, y2).
 __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __restrict__ cfg,
                                                          const uint2* __restrict__ lookup,
                                                          const uint32_t* __restrict__ offsets,
                                                          const f2* __restrict__ pred,
                                                          const f2* __restrict__ dens,
+                                                         const f2* __restrict__ pred_s,
+                                                         const f2* __restrict__ dens_s,
+                                                         const f2* __restrict__ vel_s,
                                                          const float* __restrict__ vx,
                                                          const float* __restrict__ vy,
+                                                         const float* __restrict__ x,
+                                                         const float* __restrict__ y,
                                                          float* __restrict__ vx2,
                                                          float* __restrict__ vy2,
-                                                         float* __restrict__ x,
-                                                         float* __restrict__ y, uint32_t n) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
+                                                         float* __restrict__ x2,
+                                                         float* __restrict__ y2, uint32_t p_slots) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= p_slots) return;
+  const uint32_t i = lookup[t].y;
   const float dt = cfg->fixed_delta_time;
   const float r = cfg->smoothing_radius, r2 = r * r;
   const uint32_t N = cfg->particle_count;
@@ -540,67 +601,100 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
   const float rho = rr[0], rhon = rr[1];
   const float P = (rho - td) * pm;
   const float Pn = rhon * nm;
+  const float P_rho2 = P / (rho * rho);    // loop-invariant halves of pressure_term and
+  const float Pn_rho2 = Pn / (rho * rho);  // near_pressure_term (wgsl:323-327)
   float fx = 0.0f, fy = 0.0f;
   for (int o = 0; o < 9; ++o) {
-    const uint32_t key = cell_key((int32_t)((uint32_t)cx + (uint32_t)kGridOff[o][0]),
-                                  (int32_t)((uint32_t)cy + (uint32_t)kGridOff[o][1]), N);
-    for (uint32_t j = offsets[key]; j < N; ++j) {
-      const uint2 e = lookup[j];
-      if (e.x != key) break;
-      if (e.y == i) continue;
-      const f2 q = pred[e.y];
-      const float dx = q[0] - p[0], dy = q[1] - p[1];
-      const float sq = dx * dx + dy * dy;
-      if (sq > r2) continue;
-      const float dist = sqrtf(sq);
-      float dirx, diry;
-      if (dist > 0.0001f) {
-        dirx = dx / dist;
-        diry = dy / dist;
-      } else {
-        dirx = 0.0f;
-        diry = 1.0f;
+    const uint32_t key = grid_key(cx, cy, o, N);
+    for (uint32_t j = offsets[key]; j < N; j += kScanBatch) {
+      uint2 e[kScanBatch];
+      f2 q[kScanBatch], dj[kScanBatch];
+#pragma unroll
+      for (int u = 0; u < kScanBatch; ++u) {
+        const uint32_t jj = min(j + u, N - 1u);
+        e[u] = lookup[jj];
+        q[u] = pred_s[jj];
+        dj[u] = dens_s[jj];
       }
-      const f2 dj = dens[e.y];
-      const float rj = dj[0], rnj = dj[1];
-      const float Pj = (rj - td) * pm;
-      const float Pnj = rnj * nm;
-      const float pt = (P / (rho * rho)) + (Pj / (rj * rj));
-      const float npt = (Pn / (rho * rho)) + (Pnj / (rj * rnj));
-      float dk = 0.0f, ndk = 0.0f;
-      if (!(dist >= r)) {
-        const float v = r - dist;
-        dk = (-2.0f * dn) * v;
-        ndk = ((-3.0f * ndn) * v) * v;
+      bool stop = false;
+#pragma unroll
+      for (int u = 0; u < kScanBatch; ++u) {
+        if (!stop) {
+          if (j + u >= N || e[u].x != key) {
+            stop = true;
+          } else if (e[u].y != i) {
+            const float dx = q[u][0] - p[0], dy = q[u][1] - p[1];
+            const float sq = dx * dx + dy * dy;
+            if (!(sq > r2)) {
+              const float dist = sqrtf(sq);
+              float dirx, diry;
+              if (dist > 0.0001f) {
+                dirx = dx / dist;
+                diry = dy / dist;
+              } else {
+                dirx = 0.0f;
+                diry = 1.0f;
+              }
+              const float rj = dj[u][0], rnj = dj[u][1];
+              const float Pj = (rj - td) * pm;
+              const float Pnj = rnj * nm;
+              const float pt = P_rho2 + (Pj / (rj * rj));
+              const float npt = Pn_rho2 + (Pnj / (rj * rnj));
+              float dk = 0.0f, ndk = 0.0f;
+              if (!(dist >= r)) {
+                const float v = r - dist;
+                dk = (-2.0f * dn) * v;
+                ndk = ((-3.0f * ndn) * v) * v;
+              }
+              fx = fx + (dirx * pt) * dk;
+              fy = fy + (diry * pt) * dk;
+              fx = fx + (dirx * npt) * ndk;
+              fy = fy + (diry * npt) * ndk;
+            }
+          }
+        }
       }
-      fx = fx + (dirx * pt) * dk;
-      fy = fy + (diry * pt) * dk;
-      fx = fx + (dirx * npt) * ndk;
-      fy = fy + (diry * npt) * ndk;
+      if (stop) break;
     }
   }
   float qx = vx[i] + fx * dt;
   float qy = vy[i] + fy * dt;
   float wx = 0.0f, wy = 0.0f;
   for (int o = 0; o < 9; ++o) {
-    const uint32_t key = cell_key((int32_t)((uint32_t)cx + (uint32_t)kGridOff[o][0]),
-                                  (int32_t)((uint32_t)cy + (uint32_t)kGridOff[o][1]), N);
-    for (uint32_t j = offsets[key]; j < N; ++j) {
-      const uint2 e = lookup[j];
-      if (e.x != key) break;
-      if (e.y == i) continue;
-      const f2 q = pred[e.y];
-      const float dx = p[0] - q[0], dy = p[1] - q[1];
-      const float sq = dx * dx + dy * dy;
-      if (sq > r2) continue;
-      const float dist = sqrtf(sq);
-      float k = 0.0f;
-      if (!(dist >= r)) {
-        const float v = r * r - dist * dist;
-        k = ((vn * v) * v) * v;
+    const uint32_t key = grid_key(cx, cy, o, N);
+    for (uint32_t j = offsets[key]; j < N; j += kScanBatch) {
+      uint2 e[kScanBatch];
+      f2 q[kScanBatch], vj[kScanBatch];
+#pragma unroll
+      for (int u = 0; u < kScanBatch; ++u) {
+        const uint32_t jj = min(j + u, N - 1u);
+        e[u] = lookup[jj];
+        q[u] = pred_s[jj];
+        vj[u] = vel_s[jj];
       }
-      wx = wx + (vx[e.y] - qx) * k;
-      wy = wy + (vy[e.y] - qy) * k;
+      bool stop = false;
+#pragma unroll
+      for (int u = 0; u < kScanBatch; ++u) {
+        if (!stop) {
+          if (j + u >= N || e[u].x != key) {
+            stop = true;
+          } else if (e[u].y != i) {
+            const float dx = p[0] - q[u][0], dy = p[1] - q[u][1];
+            const float sq = dx * dx + dy * dy;
+            if (!(sq > r2)) {
+              const float dist = sqrtf(sq);
+              float k = 0.0f;
+              if (!(dist >= r)) {
+                const float v = r * r - dist * dist;
+                k = ((vn * v) * v) * v;
+              }
+              wx = wx + (vj[u][0] - qx) * k;
+              wy = wy + (vj[u][1] - qy) * k;
+            }
+          }
+        }
+      }
+      if (stop) break;
     }
   }
   qx = qx + (wx * cfg->viscocity_strength) * dt;
@@ -609,8 +703,8 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
   float oy = y[i] + qy * dt;
   wall(cfg->screen_bounds[0], cfg->screen_bounds[1], cfg->screen_bounds[2], cfg->screen_bounds[3],
        cfg->damping_factor, ox, oy, qx, qy);
-  x[i] = ox;
-  y[i] = oy;
+  x2[i] = ox;
+  y2[i] = oy;
   vx2[i] = qx;
   vy2[i] = qy;
 }
@@ -755,7 +849,10 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
   *passes = stages * (stages + 1u) / 2u;
   *launches = 0;
   if (stages == 0) return hipSuccess;
-  const uint32_t tile = P < kSortTile ? P : kSortTile;
+  // Tile: 2048 entries up to P = 2^18 (enough workgroups to fill the chip in the LDS
+  // passes), 8192 above (fewer global passes; measured at 50 k / 1 M / 4 M particles).
+  const uint32_t want = P <= (1u << 18) ? 2048u : kSortTile;
+  const uint32_t tile = P < want ? P : want;
   uint32_t tile_log = 0;
   while ((1u << tile_log) < tile) ++tile_log;
   const uint32_t local_threads = tile / 2u < 1024u ? tile / 2u : 1024u;
@@ -801,14 +898,23 @@ hipError_t launch_sph_pre(const SphBuffers& b, hipStream_t s) {
                      b.y, b.vx, b.vy, b.pred, b.n);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(sph_density_kernel, dim3(blocks_for(b.n)), dim3(kBlock), 0, s, b.cfg,
-                     b.lookup, b.offsets, b.pred, b.dens, b.n);
+  hipLaunchKernelGGL(sph_gather_pv_kernel, dim3(blocks_for(b.n)), dim3(kBlock), 0, s, b.lookup,
+                     b.pred, b.vx, b.vy, b.pred_s, b.vel_s, b.n);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(sph_density_kernel, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg,
+                     b.lookup, b.offsets, b.pred, b.pred_s, b.dens, b.p);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(sph_gather_dens_kernel, dim3(blocks_for(b.n)), dim3(kBlock), 0, s, b.lookup,
+                     b.dens, b.dens_s, b.n);
   return hipGetLastError();
 }
 
 hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s) {
-  hipLaunchKernelGGL(sph_sim_kernel, dim3(blocks_for(b.n)), dim3(kBlock), 0, s, b.cfg, b.lookup,
-                     b.offsets, b.pred, b.dens, b.vx, b.vy, b.vx2, b.vy2, b.x, b.y, b.n);
+  hipLaunchKernelGGL(sph_sim_kernel, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg, b.lookup,
+                     b.offsets, b.pred, b.dens, b.pred_s, b.dens_s, b.vel_s, b.vx, b.vy, b.x, b.y,
+                     b.vx2, b.vy2, b.x2, b.y2, b.p);
   return hipGetLastError();
 }
 

@@ -1,0 +1,68 @@
+"""Throughput of the SPH and N-body modes (run on the GPU box: tools/gpu_run.sh py:tools/perf_modes.py).
+
+SPH: frames/s and particle-steps/s of the full five-pass frame (bin, bitonic, offsets,
+pre-sim, sim) at the reference default N = 50 000 and larger; N-body: interactions/s and
+TFLOP/s (20 flop/interaction convention) of the force kernel against 157.3 TF FP32."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "rust-particle-system_amd", "python"))
+
+import numpy as np  # noqa: E402
+
+import rps_amd as rps  # noqa: E402
+
+out = {}
+
+
+def sph(n, frames=50):
+    cfg = rps.default_particle_config(n)
+    # Spread the reference scatter over a domain that keeps the default density for this N.
+    scale = max(1.0, (n / 50000) ** 0.5)
+    w, h = 1920.0 * scale, 1080.0 * scale
+    cfg = rps.default_particle_config(n, screen_bounds=rps.screen_bounds_for(w, h))
+    parts = rps.setup_particles_scatter(cfg, n, seed=1)
+    with rps.Context(n, rps.MODE_SPH) as ctx:
+        ctx.set_config(cfg, rps.make_ext(shader_delay=0))
+        ctx.upload(parts)
+        ctx.step(10)
+        ctx.sync()
+        ctx.set_profiling(1)
+        ms = ctx.time_steps(frames) / frames
+        sim_ms, cnt = ctx.kernel_time()
+    r = dict(n=n, ms_per_frame=ms, frames_per_s=1e3 / ms, particle_steps_per_s=n * 1e3 / ms, sim_kernel_ms=sim_ms)
+    print("SPH", json.dumps(r), flush=True)
+    out[f"sph_{n}"] = r
+
+
+def nbody(n, steps=3):
+    cfg = rps.default_particle_config(n, gravity=0.0)
+    ext = rps.make_ext(nbody_strength=1.0, nbody_softening=1.0, shader_delay=0)
+    g = np.random.default_rng(0)
+    soa = dict(x=g.uniform(-900, 900, n).astype(np.float32), y=g.uniform(-500, 500, n).astype(np.float32),
+               vx=np.zeros(n, np.float32), vy=np.zeros(n, np.float32))
+    with rps.Context(n, rps.MODE_NBODY) as ctx:
+        ctx.set_config(cfg, ext)
+        ctx.upload_soa(soa)
+        ctx.step(1)
+        ctx.sync()
+        ctx.set_profiling(1)
+        ctx.step(steps)
+        kms, cnt = ctx.kernel_time()
+    inter = float(n) * n
+    r = dict(n=n, force_kernel_ms=kms, interactions_per_s=inter / (kms * 1e-3),
+             tflops_20=20 * inter / (kms * 1e-3) / 1e12, frac_of_157TF=20 * inter / (kms * 1e-3) / 1e12 / 157.3)
+    print("NBODY", json.dumps(r), flush=True)
+    out[f"nbody_{n}"] = r
+
+
+if __name__ == "__main__":
+    for n in (50000, 1 << 20, 1 << 22):
+        sph(n)
+    for n in (1 << 16, 1 << 18, 1 << 20):
+        nbody(n)
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "perf_modes.json"), "w") as f:
+        json.dump(out, f, indent=1)
