@@ -30,8 +30,8 @@ PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--particles", type=int, default=100_000_000, help="particles per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget")
     ap.add_argument("--cpu-sample", type=int, default=1 << 22, help="CPU-baseline particles")

@@ -74,7 +74,7 @@ struct rps_ctx {
   size_t ev_used = 0;
   // tuning
   uint32_t stream_grid = 0;  // 0: one-shot grid
-  int nontemporal = 1;
+  int nontemporal = 3;
   // comm
   ncclComm_t comm = nullptr;
   int rank = 0, nranks = 1;
@@ -418,7 +418,7 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
   ctx->global_count = global;
   ctx->ext = default_ext();
   ctx->stream_grid = (uint32_t)std::max(0, env_int("RPS_STREAM_GRID", 0));
-  ctx->nontemporal = env_int("RPS_STREAM_NT", 1) != 0;
+  ctx->nontemporal = env_int("RPS_STREAM_NT", 3) & 3;  // bit 0 loads, bit 1 stores
 
   auto bail = [&](int code) {
     std::string m = ctx->err;

@@ -14,7 +14,7 @@ struct StreamLaunch {
   int verlet;
   int lifetime;
   int stats;
-  int nontemporal;
+  int nontemporal;  // bit 0: nontemporal loads, bit 1: nontemporal stores
   uint32_t grid;  // workgroups (256 threads, 4 particles/thread/iteration)
 };
 

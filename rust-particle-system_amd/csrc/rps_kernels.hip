@@ -100,8 +100,10 @@ __device__ void block_reduce_stats(StatsAcc acc, StatsPartial* out) {
 // in place with 16-B vector accesses (4 particles per lane), grid-stride.  40 B/particle
 // with lifetime, 32 B without.
 // ---------------------------------------------------------------------------------------
-template <bool VERLET, bool LIFETIME, bool STATS, bool NT>
+// NTM: bit 0 = nontemporal loads, bit 1 = nontemporal stores.
+template <bool VERLET, bool LIFETIME, bool STATS, int NTM>
 __global__ __launch_bounds__(kBlock) void stream_step_kernel(StreamArgs a) {
+  constexpr bool NTL = (NTM & 1) != 0, NTS = (NTM & 2) != 0;
   const uint64_t nvec = a.n >> 2;
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
   const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -110,12 +112,12 @@ __global__ __launch_bounds__(kBlock) void stream_step_kernel(StreamArgs a) {
   for (uint64_t v = tid; v < nvec; v += stride) {
     const uint64_t i = v << 2;
     const uint64_t o = tidx(i);  // 4 consecutive particles never straddle a tile
-    f4 X = ld4<NT>(a.x + o);
-    f4 Y = ld4<NT>(a.y + o);
-    f4 VX = ld4<NT>(a.vx + o);
-    f4 VY = ld4<NT>(a.vy + o);
+    f4 X = ld4<NTL>(a.x + o);
+    f4 Y = ld4<NTL>(a.y + o);
+    f4 VX = ld4<NTL>(a.vx + o);
+    f4 VY = ld4<NTL>(a.vy + o);
     f4 L = {0.0f, 0.0f, 0.0f, 0.0f};
-    if constexpr (LIFETIME) L = ld4<NT>(a.life + o);
+    if constexpr (LIFETIME) L = ld4<NTL>(a.life + o);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       float x = X[c], y = Y[c], vx = VX[c], vy = VY[c], life = L[c];
@@ -127,11 +129,11 @@ __global__ __launch_bounds__(kBlock) void stream_step_kernel(StreamArgs a) {
       L[c] = life;
       if constexpr (STATS) acc.add(x, y, vx, vy, re);
     }
-    st4<NT>(a.x + o, X);
-    st4<NT>(a.y + o, Y);
-    st4<NT>(a.vx + o, VX);
-    st4<NT>(a.vy + o, VY);
-    if constexpr (LIFETIME) st4<NT>(a.life + o, L);
+    st4<NTS>(a.x + o, X);
+    st4<NTS>(a.y + o, Y);
+    st4<NTS>(a.vx + o, VX);
+    st4<NTS>(a.vy + o, VY);
+    if constexpr (LIFETIME) st4<NTS>(a.life + o, L);
   }
   // n % 4 tail particles, one per lane of the first threads.
   const uint64_t rem = a.n - (nvec << 2);
@@ -725,31 +727,33 @@ uint32_t stream_blocks_for(uint64_t n) {
   return (uint32_t)(b > 0x7FFFFFFFull ? 0x7FFFFFFFull : b);
 }
 
-template <bool V, bool L, bool S, bool NT>
+template <bool V, bool L, bool S, int NTM>
 static hipError_t launch_stream_t(const StreamArgs& a, uint32_t grid, hipStream_t s) {
-  hipLaunchKernelGGL((stream_step_kernel<V, L, S, NT>), dim3(grid), dim3(kBlock), 0, s, a);
+  hipLaunchKernelGGL((stream_step_kernel<V, L, S, NTM>), dim3(grid), dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 
+template <bool V, bool L, bool S>
+static hipError_t launch_stream_nt(const StreamArgs& a, const StreamLaunch& l, hipStream_t s) {
+  switch (l.nontemporal & 3) {
+    case 0: return launch_stream_t<V, L, S, 0>(a, l.grid, s);
+    case 1: return launch_stream_t<V, L, S, 1>(a, l.grid, s);
+    case 2: return launch_stream_t<V, L, S, 2>(a, l.grid, s);
+    default: return launch_stream_t<V, L, S, 3>(a, l.grid, s);
+  }
+}
+
 hipError_t launch_stream_step(const StreamArgs& a, const StreamLaunch& l, hipStream_t s) {
-  const int sel = (l.verlet ? 8 : 0) | (l.lifetime ? 4 : 0) | (l.stats ? 2 : 0) | (l.nontemporal ? 1 : 0);
+  const int sel = (l.verlet ? 4 : 0) | (l.lifetime ? 2 : 0) | (l.stats ? 1 : 0);
   switch (sel) {
-    case 0: return launch_stream_t<false, false, false, false>(a, l.grid, s);
-    case 1: return launch_stream_t<false, false, false, true>(a, l.grid, s);
-    case 2: return launch_stream_t<false, false, true, false>(a, l.grid, s);
-    case 3: return launch_stream_t<false, false, true, true>(a, l.grid, s);
-    case 4: return launch_stream_t<false, true, false, false>(a, l.grid, s);
-    case 5: return launch_stream_t<false, true, false, true>(a, l.grid, s);
-    case 6: return launch_stream_t<false, true, true, false>(a, l.grid, s);
-    case 7: return launch_stream_t<false, true, true, true>(a, l.grid, s);
-    case 8: return launch_stream_t<true, false, false, false>(a, l.grid, s);
-    case 9: return launch_stream_t<true, false, false, true>(a, l.grid, s);
-    case 10: return launch_stream_t<true, false, true, false>(a, l.grid, s);
-    case 11: return launch_stream_t<true, false, true, true>(a, l.grid, s);
-    case 12: return launch_stream_t<true, true, false, false>(a, l.grid, s);
-    case 13: return launch_stream_t<true, true, false, true>(a, l.grid, s);
-    case 14: return launch_stream_t<true, true, true, false>(a, l.grid, s);
-    default: return launch_stream_t<true, true, true, true>(a, l.grid, s);
+    case 0: return launch_stream_nt<false, false, false>(a, l, s);
+    case 1: return launch_stream_nt<false, false, true>(a, l, s);
+    case 2: return launch_stream_nt<false, true, false>(a, l, s);
+    case 3: return launch_stream_nt<false, true, true>(a, l, s);
+    case 4: return launch_stream_nt<true, false, false>(a, l, s);
+    case 5: return launch_stream_nt<true, false, true>(a, l, s);
+    case 6: return launch_stream_nt<true, true, false>(a, l, s);
+    default: return launch_stream_nt<true, true, true>(a, l, s);
   }
 }
 

@@ -17,7 +17,7 @@ import rps_amd as rps  # noqa: E402
 
 N = int(os.environ.get("TUNE_N", 100_000_000))
 STEPS = 50
-ROUNDS = 3
+ROUNDS = 4
 
 
 def copy_ref(nbytes):
@@ -41,9 +41,10 @@ def copy_ref(nbytes):
 
 def main():
     variants = []
-    for nt in (1, 0):
-        for grid in (0, 2048, 4096, 8192, 16384):
-            variants.append(dict(grid=grid, nt=nt, lifetime=True))
+    for nt in (3, 1, 2, 0):  # bit 0 nontemporal loads, bit 1 nontemporal stores
+        variants.append(dict(grid=0, nt=nt, lifetime=True))
+    variants.append(dict(grid=16384, nt=3, lifetime=True))
+    variants.append(dict(grid=0, nt=3, lifetime=False))
     variants.append(dict(grid=0, nt=1, lifetime=False))
     results = {json.dumps(v, sort_keys=True): [] for v in variants}
     cfg = rps.default_particle_config(N, gravity=0.0)
