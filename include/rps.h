@@ -134,7 +134,8 @@ typedef struct rps_ext_config {
   float nbody_strength;    /* all-pairs: G*m per source particle                            */
   float nbody_softening;   /* all-pairs Plummer softening epsilon                          */
   uint32_t stats_interval; /* with RPS_EXT_STATS: reduce every k-th active step (>=1)       */
-  uint32_t _pad0;
+  uint32_t fuse_steps;     /* STREAM: advance up to this many steps per launch in registers
+                              (state read/written once; bitwise == separate steps); 0/1 = off */
   rps_attractor attractors[RPS_MAX_ATTRACTORS];
 } rps_ext_config;
 

@@ -293,6 +293,45 @@ int step_stream(rps_ctx* ctx) {
   return RPS_OK;
 }
 
+// Temporal fusion (ext.fuse_steps > 1): `m` consecutive active steps starting at active-step
+// index k0 in one launch; `stats` reduces the state after the last of them.
+int step_stream_fused(rps_ctx* ctx, uint64_t k0, uint32_t m, bool stats) {
+  const rps_ext_config& e = ctx->ext;
+  FusedArgs fa;
+  std::memset(&fa, 0, sizeof(fa));
+  fa.base = make_stream_args(ctx, k0);
+  fa.nsub = m;
+  const double dt = (double)ctx->cfg.fixed_delta_time;
+  for (uint32_t sub = 0; sub < m; ++sub)
+    for (uint32_t i = 0; i < fa.base.na; ++i)
+      attractor_pos(e.attractors[i], (double)(k0 + sub) * dt, fa.ax[sub][i], fa.ay[sub][i]);
+  StreamLaunch l;
+  l.verlet = e.integrator == RPS_INTEGRATOR_VERLET;
+  l.lifetime = (e.flags & RPS_EXT_LIFETIME) != 0;
+  l.stats = stats;
+  l.nontemporal = 3;
+  const uint32_t oneshot = stream_blocks_for(ctx->n);
+  l.grid = ctx->stream_grid ? std::min(ctx->stream_grid, oneshot) : oneshot;
+  if (stats && l.grid > ctx->partial_cap) {
+    if (ctx->partials) RPS_HIP(ctx, hipFree(ctx->partials));
+    ctx->partials = nullptr;
+    RPS_HIP(ctx, hipMalloc(&ctx->partials, sizeof(StatsPartial) * (l.grid + kStatsFold)));
+    ctx->partial_cap = l.grid;
+  }
+  fa.base.partials = ctx->partials;
+  int rc = prof_begin(ctx, !stats);
+  if (rc) return rc;
+  RPS_HIP(ctx, launch_stream_fused(fa, l, ctx->stream));
+  rc = prof_end(ctx);
+  if (rc) return rc;
+  if (stats) {
+    RPS_HIP(ctx, launch_stats_finalize(ctx->partials, l.grid, ctx->partials + ctx->partial_cap,
+                                       ctx->d_stats, k0 + m - 1, ctx->stream));
+    ctx->have_stats = true;
+  }
+  return RPS_OK;
+}
+
 int step_nbody(rps_ctx* ctx) {
   const rps_config& c = ctx->cfg;
   const rps_ext_config& e = ctx->ext;
@@ -718,6 +757,11 @@ int rps_step(rps_ctx* ctx, uint32_t nsteps) {
     return fail(ctx, RPS_ERR_COMM, "sharded N-body needs rps_comm_init");
   if (ctx->mode == RPS_MODE_NBODY && ctx->global_count != ctx->n && !ctx->comm)
     return fail(ctx, RPS_ERR_COMM, "sharded N-body needs rps_comm_init");
+  const uint32_t fuse = std::min<uint32_t>(ctx->ext.fuse_steps, kMaxFuse);
+  const bool fused = ctx->mode == RPS_MODE_STREAM && fuse > 1;
+  const uint32_t interval = std::max<uint32_t>(ctx->ext.stats_interval, 1u);
+  uint32_t pending = 0;  // fused mode: active steps accumulated since the last launch
+  uint64_t pending_k0 = 0;
   for (uint32_t s = 0; s < nsteps; ++s) {
     ctx->cfg.frame_count += 1;  // src/particle_buffers.rs:227
     const bool active = ctx->cfg.frame_count >= ctx->ext.shader_delay;  // wgsl:426, :442
@@ -726,6 +770,20 @@ int rps_step(rps_ctx* ctx, uint32_t nsteps) {
       if (rc) return rc;
     }
     if (!active) continue;
+    if (fused) {
+      const uint64_t k = ctx->active_steps;
+      if (pending == 0) pending_k0 = k;
+      ++pending;
+      ++ctx->active_steps;
+      ctx->stepped = true;
+      const bool stats = (ctx->ext.flags & RPS_EXT_STATS) && (k % interval == 0);
+      if (pending == fuse || stats || s + 1 == nsteps) {
+        rc = step_stream_fused(ctx, pending_k0, pending, stats);
+        if (rc) return rc;
+        pending = 0;
+      }
+      continue;
+    }
     switch (ctx->mode) {
       case RPS_MODE_STREAM: rc = step_stream(ctx); break;
       case RPS_MODE_NBODY: rc = step_nbody(ctx); break;
@@ -735,6 +793,7 @@ int rps_step(rps_ctx* ctx, uint32_t nsteps) {
     ++ctx->active_steps;
     ctx->stepped = true;
   }
+  if (pending) return step_stream_fused(ctx, pending_k0, pending, false);
   return RPS_OK;
 }
 

@@ -73,6 +73,16 @@ struct StreamArgs {
   uint32_t key0, key1, step_lo, step_hi;
 };
 
+// Temporal fusion of up to kMaxFuse consecutive active steps in one launch: per-substep
+// attractor positions (the only per-step uniforms besides the Philox step counter).
+constexpr int kMaxFuse = 16;
+struct FusedArgs {
+  StreamArgs base;  // step_lo/step_hi = first substep's active-step index
+  uint32_t nsub;
+  float ax[kMaxFuse][kMaxAttractors];
+  float ay[kMaxFuse][kMaxAttractors];
+};
+
 struct StatsPartial {  // 48 B, written once per workgroup, reduced in fixed order
   float bbox[4];
   double ke;
@@ -206,14 +216,15 @@ __device__ __forceinline__ int32_t f32_to_i32(float v) {
 }
 
 // Sum of attractor accelerations at (x, y), attractors in index order.
-__device__ __forceinline__ void attract(const StreamArgs& a, float x, float y, float& ax,
-                                        float& ay) {
+// (apx, apy) are this step's attractor positions.
+__device__ __forceinline__ void attract(const StreamArgs& a, const float* apx, const float* apy,
+                                        float x, float y, float& ax, float& ay) {
   float sx = 0.0f, sy = 0.0f;
 #pragma unroll
   for (int k = 0; k < kMaxAttractors; ++k) {
     if ((uint32_t)k < a.na) {
-      const float dx = a.ax[k] - x;
-      const float dy = a.ay[k] - y;
+      const float dx = apx[k] - x;
+      const float dy = apy[k] - y;
       const float r2 = (dx * dx + dy * dy) + a.ae2[k];
       const float inv = 1.0f / sqrtf(r2);
       const float s = a.as[k] * ((inv * inv) * inv);
@@ -225,10 +236,11 @@ __device__ __forceinline__ void attract(const StreamArgs& a, float x, float y, f
   ay = sy;
 }
 
-__device__ __forceinline__ void respawn(const StreamArgs& a, uint64_t gid, float& x, float& y,
-                                     float& vx, float& vy, float& life) {
+__device__ __forceinline__ void respawn(const StreamArgs& a, uint64_t step, uint64_t gid, float& x,
+                                        float& y, float& vx, float& vy, float& life) {
   uint32_t w[4];
-  philox4x32_10((uint32_t)gid, (uint32_t)(gid >> 32), a.step_lo, a.step_hi, a.key0, a.key1, w);
+  philox4x32_10((uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)step, (uint32_t)(step >> 32), a.key0,
+                a.key1, w);
   const float r = a.emit_r * sqrtf(u01(w[0]));
   float c, s;
   sincos_turns(u01(w[1]), c, s);
@@ -241,8 +253,10 @@ __device__ __forceinline__ void respawn(const StreamArgs& a, uint64_t gid, float
 }
 
 // One particle, one active step.  Returns true when the particle respawned.
+// (apx, apy): attractor positions of this step; step: its active-step index (Philox counter).
 template <bool VERLET, bool LIFETIME>
-__device__ __forceinline__ bool step_one(const StreamArgs& a, uint64_t gid, float& x, float& y,
+__device__ __forceinline__ bool step_one(const StreamArgs& a, const float* apx, const float* apy,
+                                         uint64_t step, uint64_t gid, float& x, float& y,
                                          float& vx, float& vy, float& life) {
   const float dt = a.dt;
   if constexpr (!VERLET) {
@@ -250,7 +264,7 @@ __device__ __forceinline__ bool step_one(const StreamArgs& a, uint64_t gid, floa
     vy = vy + a.gy_dt;
     if (a.na) {
       float ax, ay;
-      attract(a, x, y, ax, ay);
+      attract(a, apx, apy, x, y, ax, ay);
       vx = vx + ax * dt;
       vy = vy + ay * dt;
     }
@@ -262,11 +276,11 @@ __device__ __forceinline__ bool step_one(const StreamArgs& a, uint64_t gid, floa
     y = y + vy * dt;
   } else {
     float ax0, ay0, ax1, ay1;
-    attract(a, x, y, ax0, ay0);
+    attract(a, apx, apy, x, y, ax0, ay0);
     ay0 = ay0 + a.neg_g;
     const float x1 = (x + vx * dt) + ax0 * a.half_dt2;
     const float y1 = (y + vy * dt) + ay0 * a.half_dt2;
-    attract(a, x1, y1, ax1, ay1);
+    attract(a, apx, apy, x1, y1, ax1, ay1);
     ay1 = ay1 + a.neg_g;
     vx = vx + (ax0 + ax1) * a.half_dt;
     vy = vy + (ay0 + ay1) * a.half_dt;
@@ -281,7 +295,7 @@ __device__ __forceinline__ bool step_one(const StreamArgs& a, uint64_t gid, floa
   if constexpr (LIFETIME) {
     life = life - dt;
     if (life <= 0.0f) {
-      respawn(a, gid, x, y, vx, vy, life);
+      respawn(a, step, gid, x, y, vx, vy, life);
       return true;
     }
   }

@@ -22,6 +22,7 @@ struct StreamLaunch {
 uint32_t stream_blocks_for(uint64_t n);
 
 hipError_t launch_stream_step(const StreamArgs& a, const StreamLaunch& l, hipStream_t s);
+hipError_t launch_stream_fused(const FusedArgs& a, const StreamLaunch& l, hipStream_t s);
 // Deterministic two-level reduction of per-workgroup partials (scratch: kStatsFold entries).
 constexpr uint32_t kStatsFold = 256;
 hipError_t launch_stats_finalize(const StatsPartial* partials, uint32_t count,

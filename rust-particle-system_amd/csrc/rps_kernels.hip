@@ -107,6 +107,7 @@ __global__ __launch_bounds__(kBlock) void stream_step_kernel(StreamArgs a) {
   const uint64_t nvec = a.n >> 2;
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
   const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint64_t step = ((uint64_t)a.step_hi << 32) | a.step_lo;
   StatsAcc acc;
   if constexpr (STATS) acc.init();
   for (uint64_t v = tid; v < nvec; v += stride) {
@@ -121,7 +122,8 @@ __global__ __launch_bounds__(kBlock) void stream_step_kernel(StreamArgs a) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       float x = X[c], y = Y[c], vx = VX[c], vy = VY[c], life = L[c];
-      const bool re = step_one<VERLET, LIFETIME>(a, a.id_offset + i + c, x, y, vx, vy, life);
+      const bool re = step_one<VERLET, LIFETIME>(a, a.ax, a.ay, step, a.id_offset + i + c, x, y, vx,
+                                                 vy, life);
       X[c] = x;
       Y[c] = y;
       VX[c] = vx;
@@ -142,7 +144,74 @@ __global__ __launch_bounds__(kBlock) void stream_step_kernel(StreamArgs a) {
     const uint64_t o = tidx(i);
     float x = a.x[o], y = a.y[o], vx = a.vx[o], vy = a.vy[o];
     float life = LIFETIME ? a.life[o] : 0.0f;
-    const bool re = step_one<VERLET, LIFETIME>(a, a.id_offset + i, x, y, vx, vy, life);
+    const bool re = step_one<VERLET, LIFETIME>(a, a.ax, a.ay, step, a.id_offset + i, x, y, vx, vy,
+                                               life);
+    a.x[o] = x;
+    a.y[o] = y;
+    a.vx[o] = vx;
+    a.vy[o] = vy;
+    if constexpr (LIFETIME) a.life[o] = life;
+    if constexpr (STATS) acc.add(x, y, vx, vy, re);
+  }
+  if constexpr (STATS) block_reduce_stats(acc, a.partials);
+}
+
+// Temporal fusion: the same per-particle step applied nsub times in registers, state read
+// and written once.  Particles are independent, so this is bitwise equal to
+// nsub separate launches; stats (if any) reduce the final substep's state.
+template <bool VERLET, bool LIFETIME, bool STATS, int NTM>
+__global__ __launch_bounds__(kBlock) void stream_fused_kernel(FusedArgs fa) {
+  constexpr bool NTL = (NTM & 1) != 0, NTS = (NTM & 2) != 0;
+  const StreamArgs& a = fa.base;
+  const uint64_t nvec = a.n >> 2;
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint64_t step0 = ((uint64_t)a.step_hi << 32) | a.step_lo;
+  StatsAcc acc;
+  if constexpr (STATS) acc.init();
+  for (uint64_t v = tid; v < nvec; v += stride) {
+    const uint64_t i = v << 2;
+    const uint64_t o = tidx(i);
+    f4 X = ld4<NTL>(a.x + o);
+    f4 Y = ld4<NTL>(a.y + o);
+    f4 VX = ld4<NTL>(a.vx + o);
+    f4 VY = ld4<NTL>(a.vy + o);
+    f4 L = {0.0f, 0.0f, 0.0f, 0.0f};
+    if constexpr (LIFETIME) L = ld4<NTL>(a.life + o);
+    bool re[4] = {false, false, false, false};
+    for (uint32_t sub = 0; sub < fa.nsub; ++sub) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float x = X[c], y = Y[c], vx = VX[c], vy = VY[c], life = L[c];
+        re[c] = step_one<VERLET, LIFETIME>(a, fa.ax[sub], fa.ay[sub], step0 + sub, a.id_offset + i + c,
+                                           x, y, vx, vy, life);
+        X[c] = x;
+        Y[c] = y;
+        VX[c] = vx;
+        VY[c] = vy;
+        L[c] = life;
+      }
+    }
+    if constexpr (STATS) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc.add(X[c], Y[c], VX[c], VY[c], re[c]);
+    }
+    st4<NTS>(a.x + o, X);
+    st4<NTS>(a.y + o, Y);
+    st4<NTS>(a.vx + o, VX);
+    st4<NTS>(a.vy + o, VY);
+    if constexpr (LIFETIME) st4<NTS>(a.life + o, L);
+  }
+  const uint64_t rem = a.n - (nvec << 2);
+  if (tid < rem) {
+    const uint64_t i = (nvec << 2) + tid;
+    const uint64_t o = tidx(i);
+    float x = a.x[o], y = a.y[o], vx = a.vx[o], vy = a.vy[o];
+    float life = LIFETIME ? a.life[o] : 0.0f;
+    bool re = false;
+    for (uint32_t sub = 0; sub < fa.nsub; ++sub)
+      re = step_one<VERLET, LIFETIME>(a, fa.ax[sub], fa.ay[sub], step0 + sub, a.id_offset + i, x, y, vx,
+                                      vy, life);
     a.x[o] = x;
     a.y[o] = y;
     a.vx[o] = vx;
@@ -754,6 +823,27 @@ hipError_t launch_stream_step(const StreamArgs& a, const StreamLaunch& l, hipStr
     case 5: return launch_stream_nt<true, false, true>(a, l, s);
     case 6: return launch_stream_nt<true, true, false>(a, l, s);
     default: return launch_stream_nt<true, true, true>(a, l, s);
+  }
+}
+
+template <bool V, bool L, bool S, int NTM>
+static hipError_t launch_fused_t(const FusedArgs& a, uint32_t grid, hipStream_t s) {
+  hipLaunchKernelGGL((stream_fused_kernel<V, L, S, NTM>), dim3(grid), dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+// Fused variants are built for the NT-load+store policy only (the measured best, §5).
+hipError_t launch_stream_fused(const FusedArgs& a, const StreamLaunch& l, hipStream_t s) {
+  const int sel = (l.verlet ? 4 : 0) | (l.lifetime ? 2 : 0) | (l.stats ? 1 : 0);
+  switch (sel) {
+    case 0: return launch_fused_t<false, false, false, 3>(a, l.grid, s);
+    case 1: return launch_fused_t<false, false, true, 3>(a, l.grid, s);
+    case 2: return launch_fused_t<false, true, false, 3>(a, l.grid, s);
+    case 3: return launch_fused_t<false, true, true, 3>(a, l.grid, s);
+    case 4: return launch_fused_t<true, false, false, 3>(a, l.grid, s);
+    case 5: return launch_fused_t<true, false, true, 3>(a, l.grid, s);
+    case 6: return launch_fused_t<true, true, false, 3>(a, l.grid, s);
+    default: return launch_fused_t<true, true, true, 3>(a, l.grid, s);
   }
 }
 

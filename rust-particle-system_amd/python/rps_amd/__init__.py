@@ -112,7 +112,7 @@ class ExtConfig(ctypes.Structure):
         ("nbody_strength", ctypes.c_float),
         ("nbody_softening", ctypes.c_float),
         ("stats_interval", ctypes.c_uint32),
-        ("_pad0", ctypes.c_uint32),
+        ("fuse_steps", ctypes.c_uint32),
         ("attractors", Attractor * MAX_ATTRACTORS),
     ]
 

@@ -226,3 +226,27 @@ def test_profiling_counts_dominant_kernel(gpu):
         amt, unit = ctx.step_cost()
         assert unit == "bytes" and amt == 40.0 * n
         assert ctx.time_steps(3) > 0
+
+
+@pytest.mark.parametrize("fuse,n,steps", [(4, 1 << 20, 13), (16, 65539, 40), (7, 5, 9)])
+def test_fused_steps_bitwise(gpu, orc, fuse, n, steps):
+    """ext.fuse_steps > 1: several steps per launch in registers == separate steps, bitwise;
+    stats steps close a chunk so the reduced state is the stats step's."""
+    rps = gpu
+    cfg = config_c1(rps, n)
+    ext = rps.headline_ext(stats=True)
+    ext.shader_delay = 3
+    ext.stats_interval = 5
+    ext.fuse_steps = fuse
+    soa = random_soa(n, list(cfg.screen_bounds), seed=fuse, life=(-0.05, 0.2))
+    with _gpu_ctx(rps, n, cfg, ext, soa) as ctx:
+        ctx.step(steps)
+        got = ctx.download_soa(life=True)
+        st = ctx.stats()
+        fc, act = ctx.counters()
+    ref = copy_soa(soa)
+    ofc, oact = orc.run_steps(0, cfg, ext, ref, steps)
+    assert (fc, act) == (ofc, oact)
+    assert_soa_bitwise(got, ref, keys=KEYS5)
+    last_stats = max(k for k in range(act) if k % 5 == 0)
+    assert st.step == last_stats

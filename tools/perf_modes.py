@@ -58,7 +58,27 @@ def nbody(n, steps=3):
     out[f"nbody_{n}"] = r
 
 
+def stream(n, fuse, steps=200):
+    cfg = rps.default_particle_config(min(n, 0xFFFFFFFF), gravity=0.0)
+    ext = rps.headline_ext()
+    ext.shader_delay = 0
+    ext.fuse_steps = fuse
+    with rps.Context(n) as ctx:
+        ctx.set_config(cfg, ext)
+        ctx.init_scatter()
+        ctx.step(steps // 4)
+        ctx.sync()
+        ms = ctx.time_steps(steps) / steps
+    r = dict(n=n, fuse=fuse, ms_per_step=ms, steps_per_s=1e3 / ms, updates_per_s=n * 1e3 / ms,
+             hbm_equiv_gbps=40.0 * n / (ms * 1e-3) / 1e9)
+    print("STREAM", json.dumps(r), flush=True)
+    out[f"stream_{n}_f{fuse}"] = r
+
+
 if __name__ == "__main__":
+    for n in (65536, 1 << 20, 1 << 24, 100_000_000):
+        for fuse in (1, 4, 16):
+            stream(n, fuse)
     for n in (50000, 1 << 20, 1 << 22):
         sph(n)
     for n in (1 << 16, 1 << 18, 1 << 20):
