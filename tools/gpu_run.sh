@@ -36,6 +36,8 @@ for step in "$@"; do
       run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 40 --warmup 10 --no-cpu-baseline || exit $? ;;
     prof_sph)
       run prof_sph 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_sph -o run --output-format csv -- python3 tools/sph_frames.py 50000 60 || exit $? ;;
+    prof_sph64k)
+      run prof_sph64k 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_sph64k -o run --output-format csv -- python3 tools/sph_frames.py 65536 60 || exit $? ;;
     probe)
       run hbm_probe 300 tools/hbm_probe || exit $? ;;
     *)
