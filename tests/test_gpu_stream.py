@@ -250,3 +250,32 @@ def test_fused_steps_bitwise(gpu, orc, fuse, n, steps):
     assert_soa_bitwise(got, ref, keys=KEYS5)
     last_stats = max(k for k in range(act) if k % 5 == 0)
     assert st.step == last_stats
+
+
+def test_beyond_2pow32_particles(gpu, orc):
+    """Maximum-size edge: 2^32 + 4099 particles (86 GB of tiled state in HBM).  Chunks at the
+    start, straddling global index 2^32 and at the ragged tail are checked bitwise after a
+    step: 64-bit tile addressing, the n % 4 tail and Philox counters with a non-zero high
+    word (the reference itself tops out near 4.19 M particles)."""
+    rps = gpu
+    n = (1 << 32) + 4099
+    cfg = config_c1(rps, 1 << 20)  # particle_count is u32 and informational in STREAM mode
+    ext = rps.headline_ext()
+    ext.shader_delay = 0
+    chunk = 1 << 14
+    starts = [0, (1 << 32) - chunk // 2, n - chunk]
+    fields = (rps.FIELD_X, rps.FIELD_Y, rps.FIELD_VX, rps.FIELD_VY, rps.FIELD_LIFE)
+    with rps.Context(n) as ctx:
+        ctx.set_config(cfg, ext)
+        ctx.init_scatter(seed=3)
+        ctx.step(1)
+        # force respawns inside the checked chunks
+        for s in starts:
+            ctx.upload_field(rps.FIELD_LIFE, np.full(chunk, 0.005, F), s)
+        before = [{k: ctx.download_field(f, s, chunk) for k, f in zip(KEYS5, fields)} for s in starts]
+        ctx.step(1)
+        after = [{k: ctx.download_field(f, s, chunk) for k, f in zip(KEYS5, fields)} for s in starts]
+    for s, b, a in zip(starts, before, after):
+        st = orc.stream_step(cfg, ext, b, 1, id_offset=s, stats=True)
+        assert st.respawned == chunk
+        assert_soa_bitwise(a, b, keys=KEYS5, what=f"chunk@{s} ")
