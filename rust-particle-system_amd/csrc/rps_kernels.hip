@@ -319,8 +319,8 @@ __global__ __launch_bounds__(kBlock) void field_scatter_kernel(float* field, Lay
 // Initial scatter (seeded restatement of src/main.rs:182-216)
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void init_scatter_kernel(InitArgs a) {
-  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= a.n) return;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < a.n;
+       i += (uint64_t)gridDim.x * kBlock) {
   const uint64_t g = a.id_offset + i;
   const uint64_t o = lidx(a.layout, i);
   const float t = (float)g / a.global_count_f;
@@ -340,6 +340,7 @@ __global__ __launch_bounds__(kBlock) void init_scatter_kernel(InitArgs a) {
   a.f.vx[o] = 0.0f;
   a.f.vy[o] = 0.0f;
   if (a.f.life) a.f.life[o] = a.life_min + u01(w[2]) * a.life_range;
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -789,11 +790,15 @@ inline uint32_t blocks_for(uint64_t n, uint32_t per_block = kBlock) {
 // ---------------------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------------------
+// The AQL dispatch packet counts work-items in 32 bits, so grids are capped at 2^31
+// work-items (kMaxGridBlocks x 256); kernels that can exceed it loop grid-stride.
+constexpr uint64_t kMaxGridBlocks = 1ull << 23;
+
 uint32_t stream_blocks_for(uint64_t n) {
   const uint64_t nvec = n >> 2;
   uint64_t b = (nvec + kBlock - 1) / kBlock;
   if (b == 0) b = 1;
-  return (uint32_t)(b > 0x7FFFFFFFull ? 0x7FFFFFFFull : b);
+  return (uint32_t)(b > kMaxGridBlocks ? kMaxGridBlocks : b);
 }
 
 template <bool V, bool L, bool S, int NTM>
@@ -898,7 +903,9 @@ hipError_t launch_field_scatter(float* field, Layout L, uint64_t offset, const f
 
 hipError_t launch_init_scatter(const InitArgs& a, hipStream_t s) {
   if (a.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(init_scatter_kernel, dim3(blocks_for(a.n)), dim3(kBlock), 0, s, a);
+  const uint64_t b = (a.n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(init_scatter_kernel, dim3((uint32_t)(b > kMaxGridBlocks ? kMaxGridBlocks : b)),
+                     dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 

@@ -253,12 +253,12 @@ def test_fused_steps_bitwise(gpu, orc, fuse, n, steps):
 
 
 def test_beyond_2pow32_particles(gpu, orc):
-    """Maximum-size edge: 2^32 + 4099 particles (86 GB of tiled state in HBM).  Chunks at the
+    """Maximum-size edge: 2^32 + 12291 particles (86 GB of tiled state in HBM).  Chunks at the
     start, straddling global index 2^32 and at the ragged tail are checked bitwise after a
     step: 64-bit tile addressing, the n % 4 tail and Philox counters with a non-zero high
     word (the reference itself tops out near 4.19 M particles)."""
     rps = gpu
-    n = (1 << 32) + 4099
+    n = (1 << 32) + 12291  # the straddling chunk [2^32 - 8192, 2^32 + 8192) fits; n % 4 == 3
     cfg = config_c1(rps, 1 << 20)  # particle_count is u32 and informational in STREAM mode
     ext = rps.headline_ext()
     ext.shader_delay = 0
