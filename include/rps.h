@@ -205,6 +205,11 @@ int rps_upload_particles(rps_ctx* ctx, const rps_particle* aos, uint64_t offset,
 /* SoA -> AoS download; colour derived from velocity exactly as set_color (wgsl:101-118),
  * or the spawn colour (1,1,1,1) (src/main.rs:210) before the first active step. */
 int rps_download_particles(rps_ctx* ctx, rps_particle* aos, uint64_t offset, uint64_t n);
+/* Render interop: the reference's vertex shader reads the 32-B Particle storage buffer
+ * (render_shader.wgsl:26-30, :44-45, :57).  Writes particles [offset, offset+n) in that AoS
+ * layout (colour derived exactly as set_color, wgsl:101-118) into DEVICE memory `device_dst`
+ * on the context's device, ordered on the context stream, with no host round trip. */
+int rps_export_particles(rps_ctx* ctx, rps_particle* device_dst, uint64_t offset, uint64_t n);
 /* Raw SoA field transfers (float32), for checkpoint/resume and the LIFE array. */
 int rps_upload_field(rps_ctx* ctx, int field, const float* src, uint64_t offset, uint64_t n);
 int rps_download_field(rps_ctx* ctx, int field, float* dst, uint64_t offset, uint64_t n);

@@ -651,6 +651,27 @@ int rps_download_particles(rps_ctx* ctx, rps_particle* aos, uint64_t offset, uin
   return RPS_OK;
 }
 
+int rps_export_particles(rps_ctx* ctx, rps_particle* device_dst, uint64_t offset, uint64_t n) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!device_dst && n) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "null destination");
+  if (offset + n > ctx->n) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "range exceeds particle_count");
+  if (n) {
+    hipPointerAttribute_t attr;
+    const hipError_t pe = hipPointerGetAttributes(&attr, device_dst);
+    if (pe != hipSuccess) (void)hipGetLastError();  // do not leave a sticky error for later launches
+    if (pe != hipSuccess || attr.type != hipMemoryTypeDevice)
+      return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "device_dst is not device memory");
+  }
+  constexpr uint64_t kChunk = 1ull << 30;  // stays under the 2^31 work-item grid cap
+  for (uint64_t done = 0; done < n; done += kChunk) {
+    const uint64_t m = std::min(kChunk, n - done);
+    RPS_HIP(ctx, launch_soa_to_aos(fields(ctx), ctx->layout, offset + done, device_dst + done, m,
+                                   ctx->cfg.max_energy, ctx->stepped ? 0 : 1, ctx->stream));
+  }
+  return RPS_OK;
+}
+
 int rps_upload_field(rps_ctx* ctx, int field, const float* src, uint64_t offset, uint64_t n) {
   int rc = check_ctx(ctx);
   if (rc) return rc;

@@ -162,6 +162,7 @@ ABI_SYMBOLS = [
     ("rps_get_config", _I, [_P, ctypes.POINTER(ParticleConfig), ctypes.POINTER(ExtConfig)]),
     ("rps_upload_particles", _I, [_P, _P, _U64, _U64]),
     ("rps_download_particles", _I, [_P, _P, _U64, _U64]),
+    ("rps_export_particles", _I, [_P, _P, _U64, _U64]),
     ("rps_upload_field", _I, [_P, _I, _P, _U64, _U64]),
     ("rps_download_field", _I, [_P, _I, _P, _U64, _U64]),
     ("rps_read_debug", _I, [_P, _I, _P, _U64]),
@@ -418,6 +419,11 @@ class Context:
         out = np.zeros(n, dtype=PARTICLE_DTYPE)
         self._call("rps_download_particles", _fptr(out), offset, n)
         return out
+
+    def export_particles(self, device_ptr: int, offset: int = 0, n: Optional[int] = None):
+        """Render interop: AoS Particles (render_shader.wgsl:26-30) into device memory."""
+        n = self.n - offset if n is None else n
+        self._call("rps_export_particles", ctypes.c_void_p(device_ptr), offset, n)
 
     def upload_field(self, field_id: int, values: np.ndarray, offset: int = 0):
         v = np.ascontiguousarray(values, dtype=np.float32)

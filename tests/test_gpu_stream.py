@@ -279,3 +279,32 @@ def test_beyond_2pow32_particles(gpu, orc):
         st = orc.stream_step(cfg, ext, b, 1, id_offset=s, stats=True)
         assert st.respawned == chunk
         assert_soa_bitwise(a, b, keys=KEYS5, what=f"chunk@{s} ")
+
+
+def test_render_export_matches_download(gpu):
+    """rps_export_particles writes the reference's 32-B Particle buffer (position, velocity,
+    derived colour) straight into device memory (render interop)."""
+    from hip_mem import DeviceBuffer
+
+    rps = gpu
+    n = 70001
+    cfg = config_c1(rps, n)
+    ext = rps.headline_ext()
+    ext.shader_delay = 0
+    with rps.Context(n) as ctx, DeviceBuffer(n * 32) as buf:
+        ctx.set_config(cfg, ext)
+        ctx.init_scatter()
+        ctx.export_particles(buf.ptr.value)
+        first = buf.to_host(rps.PARTICLE_DTYPE)
+        assert np.array_equal(first["color"], np.ones((n, 4), F))  # spawn colour before stepping
+        ctx.step(7)
+        ctx.export_particles(buf.ptr.value)
+        got = buf.to_host(rps.PARTICLE_DTYPE)
+        want = ctx.download()
+        assert_bitwise(got.view(np.uint32), want.view(np.uint32), "export")
+        ctx.export_particles(buf.ptr.value, offset=1000, n=500)
+        part = buf.to_host(rps.PARTICLE_DTYPE)[:500]
+        assert_bitwise(part.view(np.uint32), want[1000:1500].view(np.uint32), "export range")
+        with pytest.raises(rps.RpsError):
+            host = np.zeros(n, rps.PARTICLE_DTYPE)
+            ctx.export_particles(host.ctypes.data)  # host memory is rejected

@@ -75,7 +75,50 @@ def stream(n, fuse, steps=200):
     out[f"stream_{n}_f{fuse}"] = r
 
 
+def cpu_sph(n, frames=10):
+    """Oracle (single-thread C, -O2) SPH frames at the same N: the reference's CPU path."""
+    import time
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc
+    scale = max(1.0, (n / 50000) ** 0.5)
+    cfg = rps.default_particle_config(n, screen_bounds=rps.screen_bounds_for(1920.0 * scale, 1080.0 * scale))
+    parts = rps.setup_particles_scatter(cfg, n, seed=1)
+    soa = dict(x=parts["position"][:, 0].copy(), y=parts["position"][:, 1].copy(),
+               vx=parts["velocity"][:, 0].copy(), vy=parts["velocity"][:, 1].copy())
+    st = orc.SphState(n)
+    ext = rps.make_ext(shader_delay=0)
+    orc.run_steps(2, cfg, ext, soa, 2, sph=st)
+    t0 = time.perf_counter()
+    orc.run_steps(2, cfg, ext, soa, frames, sph=st)
+    ms = (time.perf_counter() - t0) * 1e3 / frames
+    r = dict(n=n, ms_per_frame=ms, frames_per_s=1e3 / ms, cores=1, kind="port (oracle/rps_oracle.c -O2)")
+    print("CPU_SPH", json.dumps(r), flush=True)
+    out[f"cpu_sph_{n}"] = r
+
+
+def cpu_nbody(n=8192):
+    """Oracle all-pairs (f64 accumulation, single thread) interactions/s."""
+    import time
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc
+    ext = rps.make_ext(nbody_strength=1.0, nbody_softening=1.0)
+    g = np.random.default_rng(0)
+    x = g.uniform(-900, 900, n).astype(np.float32)
+    y = g.uniform(-500, 500, n).astype(np.float32)
+    t0 = time.perf_counter()
+    orc.nbody_accel(ext, x, y)
+    el = time.perf_counter() - t0
+    r = dict(n=n, interactions_per_s=float(n) * n / el, cores=1, kind="port (oracle, f64 accumulation)")
+    print("CPU_NBODY", json.dumps(r), flush=True)
+    out[f"cpu_nbody_{n}"] = r
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "cpu":
+        cpu_sph(65536)
+        cpu_sph(1 << 20, frames=3)
+        cpu_nbody()
+        sys.exit(0)
     for n in (65536, 1 << 20, 1 << 24, 100_000_000):
         for fuse in (1, 4, 16):
             stream(n, fuse)
