@@ -51,6 +51,8 @@ struct rps_ctx {
   f2* pos_all = nullptr;
   uint64_t ns_padded = 0;
   float *ax = nullptr, *ay = nullptr;
+  f2* nb_part = nullptr;  // N-body source-split partials (nb_splits x n float2)
+  uint32_t nb_splits = 0;
   // device config (pinned upload)
   rps_config* d_cfg = nullptr;
   rps_config* h_cfg_pinned = nullptr;
@@ -347,7 +349,8 @@ int step_nbody(rps_ctx* ctx) {
   int rc = prof_begin(ctx);
   if (rc) return rc;
   RPS_HIP(ctx, launch_nbody_accel(ctx->pos_all, ctx->ns_padded, ctx->id_offset, ctx->n, eps2,
-                                  e.nbody_strength, ctx->ax, ctx->ay, ctx->stream));
+                                  e.nbody_strength, ctx->nb_part, ctx->nb_splits, ctx->ax, ctx->ay,
+                                  ctx->stream));
   rc = prof_end(ctx);
   if (rc) return rc;
   NbodyIntegrateArgs ia;
@@ -509,6 +512,9 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     slots.push_back({(void**)&ctx->pos_all, align_up(ctx->ns_padded * sizeof(f2), 256)});
     slots.push_back({(void**)&ctx->ax, nf});
     slots.push_back({(void**)&ctx->ay, nf});
+    ctx->nb_splits = nbody_splits_for(n, ctx->ns_padded);
+    if (ctx->nb_splits > 1)
+      slots.push_back({(void**)&ctx->nb_part, align_up((size_t)ctx->nb_splits * n * sizeof(f2), 256)});
   }
   slots.push_back({(void**)&ctx->d_cfg, align_up(sizeof(rps_config), 256)});
   slots.push_back({(void**)&ctx->d_stats, align_up(sizeof(StatsResult), 256)});

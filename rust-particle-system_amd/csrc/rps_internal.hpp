@@ -51,8 +51,14 @@ hipError_t launch_init_scatter(const InitArgs& a, hipStream_t s);
 constexpr uint32_t kNbodyTile = 512;  // sources staged per LDS tile (float2: 4 KiB)
 hipError_t launch_nbody_pack(const float* x, const float* y, f2* pos, uint64_t n, hipStream_t s);
 hipError_t launch_nbody_pad(f2* pos, uint64_t from, uint64_t to, hipStream_t s);
+// Source splits: enough workgroups to fill the chip (>= kNbodyMinBlocks) when the targets
+// alone are too few; each split adds nt float2 partials (part holds part_cap of them).
+constexpr uint32_t kNbodyMinBlocks = 2048;
+constexpr uint32_t kNbodyMaxSplits = 64;
+uint32_t nbody_splits_for(uint64_t nt, uint64_t ns_padded);
 hipError_t launch_nbody_accel(const f2* pos, uint64_t ns_padded, uint64_t t0, uint64_t nt,
-                              float eps2, float gm, float* ax, float* ay, hipStream_t s);
+                              float eps2, float gm, f2* part, uint32_t part_cap, float* ax,
+                              float* ay, hipStream_t s);
 struct NbodyIntegrateArgs {
   float* x;
   float* y;

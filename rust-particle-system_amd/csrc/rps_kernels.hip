@@ -359,57 +359,95 @@ __global__ __launch_bounds__(kBlock) void nbody_pad_kernel(f2* pos, uint64_t fro
   if (i < to) pos[i] = f2{1.0e18f, 1.0e18f};
 }
 
-constexpr int kTargetsPerLane = 4;
+constexpr int kTargetsPerLane = 8;
+constexpr int kTargetPairs = kTargetsPerLane / 2;
 
+// Each lane owns kTargetsPerLane targets as kTargetPairs float2 pairs (targets t and
+// t + kBlock in one pair), so every operation of the interaction except the rsq is one
+// v_pk_* instruction covering two targets: per 2 interactions 8 packed ops + 2 v_rsq_f32
+// (the FP32-VALU issue floor for this formula).  Per target the arithmetic
+// is the scalar formula r2 = dx*dx + (dy*dy + eps2) with explicit FMAs, unchanged.
+//
+// Source split (blockIdx.y): when the targets alone give too few workgroups to fill 256 CUs
+// (small N, or a strong-scaled shard), the sources are cut into gridDim.y contiguous ranges
+// of whole LDS tiles; each workgroup writes its raw partial sums to part[split][target] and
+// nbody_reduce_kernel adds them in split order (deterministic, no atomics).
 __global__ __launch_bounds__(kBlock) void nbody_accel_kernel(const f2* __restrict__ pos,
                                                              uint64_t ns_padded, uint64_t t0,
                                                              uint64_t nt, float eps2, float gm,
+                                                             uint64_t split_len,
+                                                             f2* __restrict__ part,
                                                              float* __restrict__ ax_out,
                                                              float* __restrict__ ay_out) {
   __shared__ f4 tile[kNbodyTile / 2];  // pairs of float2 sources
   const uint64_t base = (uint64_t)blockIdx.x * kBlock * kTargetsPerLane;
-  float tx[kTargetsPerLane], ty[kTargetsPerLane], ax[kTargetsPerLane], ay[kTargetsPerLane];
+  f2 tx[kTargetPairs], ty[kTargetPairs], ax[kTargetPairs], ay[kTargetPairs];
 #pragma unroll
-  for (int k = 0; k < kTargetsPerLane; ++k) {
-    const uint64_t t = base + threadIdx.x + (uint64_t)k * kBlock;
-    const f2 p = t < nt ? pos[t0 + t] : f2{0.0f, 0.0f};
-    tx[k] = p[0];
-    ty[k] = p[1];
-    ax[k] = 0.0f;
-    ay[k] = 0.0f;
+  for (int p = 0; p < kTargetPairs; ++p) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint64_t t = base + threadIdx.x + (uint64_t)(2 * p + h) * kBlock;
+      const f2 q = t < nt ? pos[t0 + t] : f2{0.0f, 0.0f};
+      tx[p][h] = q[0];
+      ty[p][h] = q[1];
+    }
+    ax[p] = f2{0.0f, 0.0f};
+    ay[p] = f2{0.0f, 0.0f};
   }
+  const f2 e2 = {eps2, eps2};
   const f4* src4 = reinterpret_cast<const f4*>(pos);
-  for (uint64_t s0 = 0; s0 < ns_padded; s0 += kNbodyTile) {
+  const uint64_t s_begin = (uint64_t)blockIdx.y * split_len;
+  const uint64_t s_end = s_begin + split_len < ns_padded ? s_begin + split_len : ns_padded;
+  for (uint64_t s0 = s_begin; s0 < s_end; s0 += kNbodyTile) {
     __syncthreads();
     for (uint32_t q = threadIdx.x; q < kNbodyTile / 2; q += kBlock) tile[q] = src4[(s0 >> 1) + q];
     __syncthreads();
-#pragma unroll 4
+#pragma unroll 2
     for (uint32_t q = 0; q < kNbodyTile / 2; ++q) {
       const f4 sp = tile[q];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const float sx = sp[2 * h], sy = sp[2 * h + 1];
+        const f2 sx = {sp[2 * h], sp[2 * h]}, sy = {sp[2 * h + 1], sp[2 * h + 1]};
 #pragma unroll
-        for (int k = 0; k < kTargetsPerLane; ++k) {
-          const float dx = sx - tx[k];
-          const float dy = sy - ty[k];
-          const float r2 = __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, eps2));
-          const float inv = __builtin_amdgcn_rsqf(r2);
-          const float inv3 = (inv * inv) * inv;
-          ax[k] = __builtin_fmaf(dx, inv3, ax[k]);
-          ay[k] = __builtin_fmaf(dy, inv3, ay[k]);
+        for (int p = 0; p < kTargetPairs; ++p) {
+          const f2 dx = sx - tx[p];
+          const f2 dy = sy - ty[p];
+          const f2 r2 = __builtin_elementwise_fma(dx, dx, __builtin_elementwise_fma(dy, dy, e2));
+          const f2 inv = {__builtin_amdgcn_rsqf(r2[0]), __builtin_amdgcn_rsqf(r2[1])};
+          const f2 inv3 = (inv * inv) * inv;
+          ax[p] = __builtin_elementwise_fma(dx, inv3, ax[p]);
+          ay[p] = __builtin_elementwise_fma(dy, inv3, ay[p]);
         }
       }
     }
   }
 #pragma unroll
-  for (int k = 0; k < kTargetsPerLane; ++k) {
-    const uint64_t t = base + threadIdx.x + (uint64_t)k * kBlock;
-    if (t < nt) {
-      ax_out[t] = ax[k] * gm;
-      ay_out[t] = ay[k] * gm;
+  for (int p = 0; p < kTargetPairs; ++p) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint64_t t = base + threadIdx.x + (uint64_t)(2 * p + h) * kBlock;
+      if (t < nt) {
+        if (part) {
+          part[(uint64_t)blockIdx.y * nt + t] = f2{ax[p][h], ay[p][h]};
+        } else {
+          ax_out[t] = ax[p][h] * gm;
+          ay_out[t] = ay[p][h] * gm;
+        }
+      }
     }
   }
+}
+
+__global__ __launch_bounds__(kBlock) void nbody_reduce_kernel(const f2* __restrict__ part,
+                                                              uint32_t splits, uint64_t nt,
+                                                              float gm, float* __restrict__ ax_out,
+                                                              float* __restrict__ ay_out) {
+  const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (t >= nt) return;
+  f2 a = part[t];
+  for (uint32_t s = 1; s < splits; ++s) a += part[(uint64_t)s * nt + t];
+  ax_out[t] = a[0] * gm;
+  ay_out[t] = a[1] * gm;
 }
 
 __global__ __launch_bounds__(kBlock) void nbody_integrate_kernel(NbodyIntegrateArgs a) {
@@ -922,11 +960,32 @@ hipError_t launch_nbody_pad(f2* pos, uint64_t from, uint64_t to, hipStream_t s) 
   return hipGetLastError();
 }
 
+uint32_t nbody_splits_for(uint64_t nt, uint64_t ns_padded) {
+  if (nt == 0) return 1;
+  const uint64_t tb = blocks_for(nt, kBlock * kTargetsPerLane);
+  const uint64_t tiles = ns_padded / kNbodyTile;
+  uint64_t s = (kNbodyMinBlocks + tb - 1) / tb;
+  if (s > kNbodyMaxSplits) s = kNbodyMaxSplits;
+  if (s > tiles) s = tiles;
+  return s < 1 ? 1u : (uint32_t)s;
+}
+
 hipError_t launch_nbody_accel(const f2* pos, uint64_t ns_padded, uint64_t t0, uint64_t nt,
-                              float eps2, float gm, float* ax, float* ay, hipStream_t s) {
+                              float eps2, float gm, f2* part, uint32_t part_cap, float* ax,
+                              float* ay, hipStream_t s) {
   if (nt == 0) return hipSuccess;
-  hipLaunchKernelGGL(nbody_accel_kernel, dim3(blocks_for(nt, kBlock * kTargetsPerLane)),
-                     dim3(kBlock), 0, s, pos, ns_padded, t0, nt, eps2, gm, ax, ay);
+  uint32_t splits = nbody_splits_for(nt, ns_padded);
+  if (splits > part_cap) splits = part_cap;
+  const uint64_t tiles = ns_padded / kNbodyTile;
+  const uint64_t split_len = (tiles + splits - 1) / splits * kNbodyTile;
+  splits = (uint32_t)((ns_padded + split_len - 1) / split_len);  // no empty split
+  f2* p = splits > 1 ? part : nullptr;
+  hipLaunchKernelGGL(nbody_accel_kernel, dim3(blocks_for(nt, kBlock * kTargetsPerLane), splits),
+                     dim3(kBlock), 0, s, pos, ns_padded, t0, nt, eps2, gm, split_len, p, ax, ay);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !p) return e;
+  hipLaunchKernelGGL(nbody_reduce_kernel, dim3(blocks_for(nt)), dim3(kBlock), 0, s, p, splits, nt, gm,
+                     ax, ay);
   return hipGetLastError();
 }
 

@@ -10,6 +10,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <utility>
 #include <vector>
 
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -103,6 +104,66 @@ __global__ __launch_bounds__(256) void rmw5_tiled_u_k(f4* base, size_t n4, float
   }
 }
 
+// XCD-aware block order: blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md
+// "Workgroup dispatch"), so remap b -> a contiguous chunk per XCD (bijection for any G).
+__device__ __forceinline__ size_t xcd_block(size_t b, size_t G) {
+  const size_t q = G / 8, r = G % 8, x = b % 8, k = b / 8;
+  return x * q + (x < r ? x : r) + k;
+}
+
+// Tiled, optional XCD remap, optional ping-pong (read src tiles, write dst tiles).
+template <bool NT, int T, bool XCD, bool PP>
+__global__ __launch_bounds__(256) void rmw5_tiled_x_k(f4* src, f4* dst, size_t n4, float s) {
+  const size_t b = XCD ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+  size_t v = b * 256 + threadIdx.x;
+  if (v >= n4) return;
+  constexpr size_t T4 = T / 4;
+  const size_t tile = v / T4, w = v % T4;
+  const size_t off = tile * 5 * T4 + w;
+  const f4* t = src + off;
+  f4* u = (PP ? dst : src) + off;
+  f4 A = ld<NT>(t), B = ld<NT>(t + T4), C = ld<NT>(t + 2 * T4), D = ld<NT>(t + 3 * T4), E = ld<NT>(t + 4 * T4);
+  st<NT>(u, A * s + B);
+  st<NT>(u + T4, B * s + C);
+  st<NT>(u + 2 * T4, C * s + D);
+  st<NT>(u + 3 * T4, D * s + E);
+  st<NT>(u + 4 * T4, E * s + A);
+}
+
+// Flat in-place float4 update (one stream, field-agnostic) over the same 5n-float buffer.
+template <bool NT>
+__global__ __launch_bounds__(256) void flat_rmw_k(f4* a, size_t n4, float s) {
+  size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n4) st<NT>(a + i, ld<NT>(a + i) * s + 1.0f);
+}
+
+// Flat, U float4 per lane spaced by the grid's wave slice (loads first, then stores).
+template <bool NT, int U>
+__global__ __launch_bounds__(256) void flat_rmw_u_k(f4* a, size_t n4, float s) {
+  const size_t base = (size_t)blockIdx.x * 256 * U + threadIdx.x;
+  f4 r[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) if (base + u * 256 < n4) r[u] = ld<NT>(a + base + u * 256);
+#pragma unroll
+  for (int u = 0; u < U; ++u) if (base + u * 256 < n4) st<NT>(a + base + u * 256, r[u] * s + 1.0f);
+}
+
+// Same with 512-thread workgroups.
+template <bool NT, int T>
+__global__ __launch_bounds__(512) void rmw5_tiled_b512_k(f4* base, size_t n4, float s) {
+  size_t v = (size_t)blockIdx.x * 512 + threadIdx.x;
+  if (v >= n4) return;
+  constexpr size_t T4 = T / 4;
+  const size_t tile = v / T4, w = v % T4;
+  f4* t = base + tile * 5 * T4 + w;
+  f4 A = ld<NT>(t), B = ld<NT>(t + T4), C = ld<NT>(t + 2 * T4), D = ld<NT>(t + 3 * T4), E = ld<NT>(t + 4 * T4);
+  st<NT>(t, A * s + B);
+  st<NT>(t + T4, B * s + C);
+  st<NT>(t + 2 * T4, C * s + D);
+  st<NT>(t + 3 * T4, D * s + E);
+  st<NT>(t + 4 * T4, E * s + A);
+}
+
 template <bool NT>
 __global__ __launch_bounds__(256) void rmw4_k(f4* a, f4* b, f4* c, f4* d, size_t n4, float s) {
   size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
@@ -177,8 +238,26 @@ int main(int argc, char** argv) {
   f4* tb;
   CHECK(hipMalloc(&tb, 5 * n * sizeof(float)));
   CHECK(hipMemset(tb, 0, 5 * n * sizeof(float)));
+  f4* tb2;
+  CHECK(hipMalloc(&tb2, 5 * n * sizeof(float)));
+  CHECK(hipMemset(tb2, 0, 5 * n * sizeof(float)));
+  const bool only_new = argc > 2;
   for (int round = 0; round < 2; ++round) {
     std::printf("-- round %d (n = %zu floats/array)\n", round, n);
+    run("t8192 nt", 40.0 * n, [&] { hipLaunchKernelGGL((rmw5_tiled_k<true, 8192>), dim3(g), dim3(256), 0, 0, tb, n4, 1.0f); });
+    run("t8192 xcd", 40.0 * n, [&] { hipLaunchKernelGGL((rmw5_tiled_x_k<true, 8192, true, false>), dim3(g), dim3(256), 0, 0, tb, tb, n4, 1.0f); });
+    run("pp8192 nt", 40.0 * n, [&] { hipLaunchKernelGGL((rmw5_tiled_x_k<true, 8192, false, true>), dim3(g), dim3(256), 0, 0, tb, tb2, n4, 1.0f); std::swap(tb, tb2); });
+    run("pp8192 xcd", 40.0 * n, [&] { hipLaunchKernelGGL((rmw5_tiled_x_k<true, 8192, true, true>), dim3(g), dim3(256), 0, 0, tb, tb2, n4, 1.0f); std::swap(tb, tb2); });
+    run("pp65536 nt", 40.0 * n, [&] { hipLaunchKernelGGL((rmw5_tiled_x_k<true, 65536, false, true>), dim3(g), dim3(256), 0, 0, tb, tb2, n4, 1.0f); std::swap(tb, tb2); });
+    run("t8192 b512", 40.0 * n, [&] { hipLaunchKernelGGL((rmw5_tiled_b512_k<true, 8192>), dim3((g + 1) / 2), dim3(512), 0, 0, tb, n4, 1.0f); });
+    run("copy5 nt", 40.0 * n, [&] { hipLaunchKernelGGL(copy5_k<true>, dim3(g), dim3(256), 0, 0, a, b, c, d, e, a2, b2, c2, d2, e2, n4, 1.0f); });
+    const size_t f4n = 5 * n4;
+    const unsigned gf = (unsigned)((f4n + 255) / 256);
+    run("flat rmw", 40.0 * n, [&] { hipLaunchKernelGGL(flat_rmw_k<true>, dim3(gf), dim3(256), 0, 0, tb, f4n, 1.0f); });
+    run("flat rmw u5", 40.0 * n, [&] { hipLaunchKernelGGL((flat_rmw_u_k<true, 5>), dim3((gf + 4) / 5), dim3(256), 0, 0, tb, f4n, 1.0f); });
+    run("flat rmw u4", 40.0 * n, [&] { hipLaunchKernelGGL((flat_rmw_u_k<true, 4>), dim3((gf + 3) / 4), dim3(256), 0, 0, tb, f4n, 1.0f); });
+    run("flat copy", 40.0 * n, [&] { hipLaunchKernelGGL(copy_k<true>, dim3(gf), dim3(256), 0, 0, tb, tb2, f4n); std::swap(tb, tb2); });
+    if (only_new) continue;
     run("rmw5 nt", 40.0 * n, [&] { hipLaunchKernelGGL(rmw5_k<true>, dim3(g), dim3(256), 0, 0, a, b, c, d, e, n4, 1.0f); });
     run("t1024 nt", 40.0 * n, [&] { hipLaunchKernelGGL((rmw5_tiled_k<true, 1024>), dim3(g), dim3(256), 0, 0, tb, n4, 1.0f); });
     run("t2048 nt", 40.0 * n, [&] { hipLaunchKernelGGL((rmw5_tiled_k<true, 2048>), dim3(g), dim3(256), 0, 0, tb, n4, 1.0f); });
