@@ -39,6 +39,11 @@ def parse():
     ap.add_argument("--seed", type=int, default=0x5EED)
     ap.add_argument("--profile-every", type=int, default=8,
                     help="bracket every k-th kernel launch with HIP events (roofline.achieved)")
+    ap.add_argument("--allpairs-n", type=int, default=1 << 22,
+                    help="global particles of the all-pairs N-body side measurement (0: skip)")
+    ap.add_argument("--allpairs-steps", type=int, default=2)
+    ap.add_argument("--allpairs-timeout", type=float, default=240.0,
+                    help="watchdog: print the headline line and exit if the side run hangs")
     return ap.parse_args()
 
 
@@ -70,6 +75,13 @@ class Dist:
     def sync_device(self):
         if self.dist and self.backend == "nccl":
             self.torch.cuda.synchronize()
+
+    def broadcast_bytes(self, b: bytes) -> bytes:
+        if not self.dist:
+            return b
+        obj = [b if self.rank == 0 else None]
+        self.dist.broadcast_object_list(obj, src=0)
+        return obj[0]
 
     def max(self, v: float) -> float:
         if not self.dist:
@@ -121,6 +133,50 @@ def cpu_baseline(rps, args, cfg, ext):
     return {"value": n * steps / el, "unit": "particle-updates/s", "cores": threads, "kind": "port",
             "sample": f"{n} particles x {steps} steps of the C3 step (oracle/rps_oracle.c, -O3 -fopenmp, "
                       f"{threads} threads), {el:.1f} s"}
+
+
+def allpairs(rps, args, d):
+    """Side measurement (north_star C4/C5 shape, strong scaling): all-pairs softened gravity
+    over `allpairs_n` global particles (A11 scatter), targets index-sharded over the ranks,
+    sources = every particle via the library's in-place ncclAllGather of float2 positions
+    over xGMI each step.  Not the headline `value`; reported under "allpairs"."""
+    ng = args.allpairs_n
+    if ng % d.world:
+        raise ValueError("allpairs_n must divide by the world size")
+    n = ng // d.world
+    cfg = rps.default_particle_config(min(ng, 0xFFFFFFFF), gravity=0.0)
+    ext = rps.make_ext(nbody_strength=1.0e5, nbody_softening=1.0, shader_delay=0)
+    ctx = rps.Context(n, rps.MODE_NBODY, device=d.local if d.dist else 0, id_offset=d.rank * n,
+                      global_count=ng)
+    try:
+        ctx.set_config(cfg, ext)
+        if d.world > 1:
+            ctx.comm_init(d.rank, d.world, d.broadcast_bytes(rps.comm_unique_id() if d.rank == 0 else b""))
+        ctx.init_scatter(args.seed)
+        ctx.step(1)  # warm: RCCL channels, LDS kernels
+        ctx.sync()
+        d.sync_device()
+        d.barrier()
+        ctx.set_profiling(1)
+        t0 = time.perf_counter()
+        ctx.step(args.allpairs_steps)
+        ctx.sync()
+        d.sync_device()
+        t1 = time.perf_counter()
+        d.barrier()
+        el = d.max(t1 - t0)
+        kms, _ = ctx.kernel_time()
+        kms = d.max(kms)
+    finally:
+        ctx.close()
+    inter = float(ng) * ng * args.allpairs_steps
+    flop = 20.0 * float(n) * ng  # per rank per step (GPU Gems 3 convention, rsqrt = 4)
+    return {"workload": f"all-pairs softened gravity, {ng} global particles, index-sharded x{d.world}",
+            "scaling": "strong", "steps": args.allpairs_steps, "ms_per_step": el * 1e3 / args.allpairs_steps,
+            "interactions_per_s": inter / el, "force_kernel_ms": kms,
+            "roofline": {"bound": "valu", "achieved": flop / (kms * 1e-3) / 1e12, "peak": 157.3,
+                         "unit": "TFLOP/s", "frac": flop / (kms * 1e-3) / 1e12 / 157.3},
+            "collective": f"ncclAllGather {8 * ng} B per step" if d.world > 1 else "none (1 rank)"}
 
 
 def main():
@@ -184,6 +240,23 @@ def main():
     }
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(rps, args, cfg, ext)
+    if args.allpairs_n > 0:
+        import threading
+
+        def _watchdog():  # a hung side run must not cost the headline line
+            if d.rank == 0:
+                line["allpairs"] = {"error": f"watchdog: no result within {args.allpairs_timeout} s"}
+                print(json.dumps(line), flush=True)
+            os._exit(0)
+
+        timer = threading.Timer(args.allpairs_timeout, _watchdog)
+        timer.daemon = True
+        timer.start()
+        try:
+            line["allpairs"] = allpairs(rps, args, d)
+        except Exception as ex:  # report, keep the headline
+            line["allpairs"] = {"error": f"{type(ex).__name__}: {ex}"}
+        timer.cancel()
     if d.rank == 0:
         print(json.dumps(line), flush=True)
     d.close()
