@@ -114,7 +114,7 @@ typedef enum rps_integrator {
 } rps_integrator;
 
 enum {
-  RPS_EXT_LIFETIME = 1u << 0, /* keep a life array; life -= dt; respawn at the emitter when <= 0 */
+  RPS_EXT_LIFETIME = 1u << 0, /* lifetime in whole steps; respawn at the emitter on expiry (below) */
   RPS_EXT_STATS = 1u << 1     /* fuse bbox / kinetic-energy / respawn-count reductions into the step */
 };
 
@@ -164,13 +164,15 @@ typedef enum rps_field {
   RPS_FIELD_Y = 1,
   RPS_FIELD_VX = 2,
   RPS_FIELD_VY = 3,
-  RPS_FIELD_LIFE = 4,
+  RPS_FIELD_LIFE = 4,        /* seconds = LIFE_STEPS * dt (STREAM)                  */
+  RPS_FIELD_LIFE_STEPS = 5,  /* whole lifetime steps left, an exact f32 integer      */
   RPS_DEBUG_SPATIAL_LOOKUP = 16,  /* u32x2 (key, index) x next_pow2(N)   (wgsl:52)  */
   RPS_DEBUG_LOOKUP_OFFSETS = 17,  /* u32 x N                              (wgsl:55)  */
   RPS_DEBUG_DENSITIES = 18,       /* f32x2 (density, near) x N            (wgsl:58)  */
   RPS_DEBUG_PREDICTED = 19,       /* f32x2 x N                            (wgsl:61)  */
   RPS_DEBUG_ACCEL_X = 20,         /* f32 x N  N-body acceleration (build-defined)    */
-  RPS_DEBUG_ACCEL_Y = 21          /* f32 x N                                          */
+  RPS_DEBUG_ACCEL_Y = 21,         /* f32 x N                                          */
+  RPS_DEBUG_EXPIRY = 22           /* u16 x N  lifetime expiry (STREAM) */
 } rps_field;
 
 typedef struct rps_stats {
@@ -210,7 +212,12 @@ int rps_download_particles(rps_ctx* ctx, rps_particle* aos, uint64_t offset, uin
  * layout (colour derived exactly as set_color, wgsl:101-118) into DEVICE memory `device_dst`
  * on the context's device, ordered on the context stream, with no host round trip. */
 int rps_export_particles(rps_ctx* ctx, rps_particle* device_dst, uint64_t offset, uint64_t n);
-/* Raw SoA field transfers (float32), for checkpoint/resume and the LIFE array. */
+/* Raw SoA field transfers (float32), for checkpoint/resume.  The lifetime (STREAM) is not
+ * stored as seconds: each particle keeps a u16 expiry e, the lifetime-clock value c (= active
+ * steps run with RPS_EXT_LIFETIME on) of the step in which it respawns, so it has
+ * (u16)(e - c) + 1 steps left.  RPS_FIELD_LIFE_STEPS reads that count (exact; checkpoints) and
+ * writes e = c + clamp(ceil(v), 1, 65535) - 1; RPS_FIELD_LIFE reads steps * dt seconds and
+ * writes L seconds as clamp(ceil(L / dt), 1, 65535) steps. */
 int rps_upload_field(rps_ctx* ctx, int field, const float* src, uint64_t offset, uint64_t n);
 int rps_download_field(rps_ctx* ctx, int field, float* dst, uint64_t offset, uint64_t n);
 /* Debug readback of SPH intermediates (src/debug.rs:121-265); bytes must equal the buffer. */
@@ -218,7 +225,8 @@ int rps_read_debug(rps_ctx* ctx, int which, void* dst, uint64_t bytes);
 
 /* Device-side initial scatter, a seeded restatement of setup_particles_scatter
  * (src/main.rs:182-216): x linear in the global id, y ~ Normal(centre, 0.125 H) clamped,
- * v = 0, life ~ U(life_min, life_max).  Uses the current config's screen_bounds. */
+ * v = 0, life ~ U(life_min, life_max) (kept as an expiry, see RPS_FIELD_LIFE).  Uses the
+ * current config's screen_bounds. */
 int rps_init_scatter(rps_ctx* ctx, uint64_t seed);
 
 /* == ParticleComputeNode::run (src/particle_compute.rs:91-195), nsteps times.  Each step

@@ -44,9 +44,12 @@ def lib(omp: bool = False) -> ctypes.CDLL:
         "orc_hash_cell": (_U32, [ctypes.c_int32, ctypes.c_int32]),
         "orc_cell_key": (_U32, [ctypes.c_int32, ctypes.c_int32, _U32]),
         "orc_f32_to_i32": (ctypes.c_int32, [_F]),
-        "orc_stream_step": (None, [_P, _P, _U64, _U64, _P, _P, _P, _P, _P, _U64, _P]),
-        "orc_stream_step_omp": (None, [_P, _P, _U64, _U64, _P, _P, _P, _P, _P, _U64, _I]),
-        "orc_init_scatter": (None, [_P, _P, _U64, _U64, _U64, _P, _P, _P, _P, _P, _U64]),
+        "orc_life_steps": (_U32, [_F, _F]),
+        "orc_exp_from_life": (None, [_P, _U64, _U32, _F, _P]),
+        "orc_life_from_exp": (None, [_P, _U64, _U32, _F, _P]),
+        "orc_stream_step": (None, [_P, _P, _U64, _U64, _U32, _P, _P, _P, _P, _P, _U64, _P]),
+        "orc_stream_step_omp": (None, [_P, _P, _U64, _U64, _U32, _P, _P, _P, _P, _P, _U64, _I]),
+        "orc_init_scatter": (None, [_P, _P, _U64, _U64, _U64, _U32, _P, _P, _P, _P, _P, _U64]),
         "orc_nbody_accel": (None, [_P, _P, _P, _U64, _U64, _U64, _P, _P]),
         "orc_nbody_integrate": (None, [_P, _P, _P, _P, _P, _P, _P, _P, _U64]),
         "orc_sph_bin": (None, [_P, _P, _P, _P, _P, _U32]),
@@ -112,31 +115,78 @@ def set_color_array(vx, vy, max_energy):
     return out
 
 
-def stream_step(cfg, ext, soa, active_step, id_offset=0, stats=False):
-    """One active stream step in place on soa = dict(x, y, vx, vy[, life]) float32 arrays."""
-    life = soa.get("life")
-    use_life = life is not None and (ext.flags & 1)
+def life_steps(life, dt):
+    return lib().orc_life_steps(life, dt)
+
+
+def exp_from_life(life, clock, dt):
+    """Lifetime expiries (u16) of `life` seconds written at lifetime clock `clock`."""
+    life = np.ascontiguousarray(life, np.float32)
+    out = np.zeros(len(life), np.uint16)
+    lib().orc_exp_from_life(_p(life), len(life), clock & 0xFFFFFFFF, dt, _p(out))
+    return out
+
+
+def life_from_exp(exp, clock, dt):
+    """Life in seconds read at lifetime clock `clock` (the clock of the next step)."""
+    exp = np.ascontiguousarray(exp, np.uint16)
+    out = np.zeros(len(exp), np.float32)
+    lib().orc_life_from_exp(_p(exp), len(exp), clock & 0xFFFFFFFF, dt, _p(out))
+    return out
+
+
+def exp_from_steps(steps, clock):
+    """Expiries of particles with `steps` (>= 1) lifetime steps left before clock `clock`."""
+    st = np.clip(np.ceil(np.asarray(steps, np.float32)), 1, 65535).astype(np.uint32)
+    return ((np.uint32(clock & 0xFFFFFFFF) + st - np.uint32(1)) & np.uint32(0xFFFF)).astype(np.uint16)
+
+
+def steps_from_exp(exp, clock):
+    left = (np.asarray(exp, np.uint32) - np.uint32(clock & 0xFFFF)) & np.uint32(0xFFFF)
+    return (left + np.uint32(1)).astype(np.float32)
+
+
+def _exp_of(soa, cfg, clock):
+    """The soa's u16 expiry array, created from its `life` view on first use (at `clock`, the
+    lifetime clock at which the GPU side received the same life values)."""
+    if soa.get("exp") is None and soa.get("life") is not None:
+        soa["exp"] = exp_from_life(soa["life"], clock, cfg.fixed_delta_time)
+    return soa.get("exp")
+
+
+def stream_step(cfg, ext, soa, active_step, id_offset=0, stats=False, clock=None):
+    """One active stream step in place on soa = dict(x, y, vx, vy[, life / exp]) arrays.
+    clock: this step's lifetime clock (default: active_step, i.e. lifetime on since step 0).
+    With lifetime on, soa["exp"] (u16) is the state and soa["life"] its seconds view."""
+    clock = active_step if clock is None else clock
+    use_life = bool(ext.flags & 1) and (soa.get("life") is not None or soa.get("exp") is not None)
+    exp = _exp_of(soa, cfg, clock) if use_life else None
     st = OrcStats() if stats else None
-    lib().orc_stream_step(_ref(cfg), _ref(ext), id_offset, active_step, _p(soa["x"]), _p(soa["y"]),
-                          _p(soa["vx"]), _p(soa["vy"]), _p(life) if use_life else None,
-                          len(soa["x"]), _ref(st) if st is not None else None)
+    lib().orc_stream_step(_ref(cfg), _ref(ext), id_offset, active_step, clock & 0xFFFFFFFF, _p(soa["x"]),
+                          _p(soa["y"]), _p(soa["vx"]), _p(soa["vy"]), _p(exp), len(soa["x"]),
+                          _ref(st) if st is not None else None)
+    if use_life:
+        soa["life"] = life_from_exp(exp, clock + 1, cfg.fixed_delta_time)
     return st
 
 
-def stream_step_omp(cfg, ext, soa, active_step, id_offset=0, threads=0):
-    life = soa.get("life")
-    use_life = life is not None and (ext.flags & 1)
-    lib(omp=True).orc_stream_step_omp(_ref(cfg), _ref(ext), id_offset, active_step, _p(soa["x"]),
-                                      _p(soa["y"]), _p(soa["vx"]), _p(soa["vy"]),
-                                      _p(life) if use_life else None, len(soa["x"]), threads)
+def stream_step_omp(cfg, ext, soa, active_step, id_offset=0, threads=0, clock=None):
+    """Same as stream_step, OpenMP build (bench cpu_baseline); the life view is not refreshed."""
+    clock = active_step if clock is None else clock
+    use_life = bool(ext.flags & 1) and (soa.get("life") is not None or soa.get("exp") is not None)
+    exp = _exp_of(soa, cfg, clock) if use_life else None
+    lib(omp=True).orc_stream_step_omp(_ref(cfg), _ref(ext), id_offset, active_step, clock & 0xFFFFFFFF,
+                                      _p(soa["x"]), _p(soa["y"]), _p(soa["vx"]), _p(soa["vy"]),
+                                      _p(exp), len(soa["x"]), threads)
 
 
-def init_scatter(cfg, ext, seed, n, id_offset=0, global_count=None, life=True):
+def init_scatter(cfg, ext, seed, n, id_offset=0, global_count=None, life=True, clock=0):
     global_count = global_count or (id_offset + n)
     soa = {k: np.zeros(n, np.float32) for k in ("x", "y", "vx", "vy")}
-    soa["life"] = np.zeros(n, np.float32) if life else None
-    lib().orc_init_scatter(_ref(cfg), _ref(ext), seed, id_offset, global_count, _p(soa["x"]),
-                           _p(soa["y"]), _p(soa["vx"]), _p(soa["vy"]), _p(soa["life"]), n)
+    soa["exp"] = np.zeros(n, np.uint16) if life else None
+    lib().orc_init_scatter(_ref(cfg), _ref(ext), seed, id_offset, global_count, clock & 0xFFFFFFFF,
+                           _p(soa["x"]), _p(soa["y"]), _p(soa["vx"]), _p(soa["vy"]), _p(soa["exp"]), n)
+    soa["life"] = life_from_exp(soa["exp"], clock, cfg.fixed_delta_time) if life else None
     return soa
 
 

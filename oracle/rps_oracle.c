@@ -157,6 +157,7 @@ typedef struct step_consts {
   float ax[RPS_MAX_ATTRACTORS], ay[RPS_MAX_ATTRACTORS];
   float as[RPS_MAX_ATTRACTORS], ae2[RPS_MAX_ATTRACTORS];
   uint32_t key0, key1, step_lo, step_hi;
+  uint32_t clock; /* lifetime clock of this step */
 } step_consts;
 
 static void make_consts(const rps_config* cfg, const rps_ext_config* ext, uint64_t active_step,
@@ -202,8 +203,26 @@ static inline void attract(const step_consts* k, float x, float y, float* ax, fl
   *ay = sy;
 }
 
-static inline void respawn(const rps_ext_config* ext, const step_consts* k, uint64_t gid,
-                           float* x, float* y, float* vx, float* vy, float* life) {
+/* Lifetime in whole steps: clamp(ceil(L / dt), 1, 65535). */
+uint32_t orc_life_steps(float life, float dt) {
+  float q = ceilf(life / dt);
+  if (!(q >= 1.0f)) return 1u;
+  if (q >= 65535.0f) return 65535u;
+  return (uint32_t)q;
+}
+
+/* life (seconds) <-> expiry at lifetime clock c: e = c + steps(L) - 1; L = ((u16)(e-c)+1)*dt. */
+void orc_exp_from_life(const float* life, uint64_t n, uint32_t clock, float dt, uint16_t* exp) {
+  for (uint64_t i = 0; i < n; ++i) exp[i] = (uint16_t)(clock + orc_life_steps(life[i], dt) - 1u);
+}
+void orc_life_from_exp(const uint16_t* exp, uint64_t n, uint32_t clock, float dt, float* life) {
+  for (uint64_t i = 0; i < n; ++i)
+    life[i] = (float)((uint32_t)(uint16_t)(exp[i] - (uint16_t)clock) + 1u) * dt;
+}
+
+/* Returns the new lifetime in steps. */
+static inline uint32_t respawn(const rps_ext_config* ext, const step_consts* k, uint64_t gid,
+                               float* x, float* y, float* vx, float* vy) {
   uint32_t ctr[4] = {(uint32_t)gid, (uint32_t)(gid >> 32), k->step_lo, k->step_hi};
   uint32_t key[2] = {k->key0, k->key1};
   uint32_t w[4];
@@ -216,13 +235,13 @@ static inline void respawn(const rps_ext_config* ext, const step_consts* k, uint
   float spd = ext->spawn_speed_min + u01(w[3]) * (ext->spawn_speed_max - ext->spawn_speed_min);
   *vx = spd * c;
   *vy = spd * s;
-  *life = ext->life_min + u01(w[2]) * (ext->life_max - ext->life_min);
+  return orc_life_steps(ext->life_min + u01(w[2]) * (ext->life_max - ext->life_min), k->dt);
 }
 
 /* Returns 1 if the particle respawned. */
 static inline int stream_one(const rps_config* cfg, const rps_ext_config* ext,
                              const step_consts* k, uint64_t gid, float* px, float* py,
-                             float* pvx, float* pvy, float* plife) {
+                             float* pvx, float* pvy, uint16_t* pexp) {
   float x = *px, y = *py, vx = *pvx, vy = *pvy;
   const float dt = k->dt;
   if (!k->verlet) {
@@ -262,13 +281,9 @@ static inline int stream_one(const rps_config* cfg, const rps_ext_config* ext,
   /* check_screen_bounds (wgsl:69-99) */
   wall(cfg, &x, &y, &vx, &vy);
   int re = 0;
-  if (k->lifetime) {
-    float life = *plife - dt;
-    if (life <= 0.0f) {
-      respawn(ext, k, gid, &x, &y, &vx, &vy, &life);
-      re = 1;
-    }
-    *plife = life;
+  if (k->lifetime && *pexp == (uint16_t)k->clock) { /* expiry reached: respawn */
+    *pexp = (uint16_t)(k->clock + respawn(ext, k, gid, &x, &y, &vx, &vy));
+    re = 1;
   }
   *px = x;
   *py = y;
@@ -278,17 +293,18 @@ static inline int stream_one(const rps_config* cfg, const rps_ext_config* ext,
 }
 
 void orc_stream_step(const rps_config* cfg, const rps_ext_config* ext, uint64_t id_offset,
-                     uint64_t active_step, float* x, float* y, float* vx, float* vy,
-                     float* life, uint64_t n, orc_stats* stats) {
+                     uint64_t active_step, uint32_t clock, float* x, float* y, float* vx,
+                     float* vy, uint16_t* exp, uint64_t n, orc_stats* stats) {
   step_consts k;
   make_consts(cfg, ext, active_step, &k);
-  if (!life) k.lifetime = 0;
+  k.clock = clock;
+  if (!exp) k.lifetime = 0;
   float bx0 = INFINITY, bx1 = -INFINITY, by0 = INFINITY, by1 = -INFINITY;
   double ke = 0.0;
   uint64_t re = 0;
   for (uint64_t i = 0; i < n; ++i) {
     re += (uint64_t)stream_one(cfg, ext, &k, id_offset + i, &x[i], &y[i], &vx[i], &vy[i],
-                               k.lifetime ? &life[i] : NULL);
+                               k.lifetime ? &exp[i] : NULL);
     if (stats) {
       bx0 = x[i] < bx0 ? x[i] : bx0;
       bx1 = x[i] > bx1 ? x[i] : bx1;
@@ -309,18 +325,19 @@ void orc_stream_step(const rps_config* cfg, const rps_ext_config* ext, uint64_t 
 }
 
 void orc_stream_step_omp(const rps_config* cfg, const rps_ext_config* ext, uint64_t id_offset,
-                         uint64_t active_step, float* x, float* y, float* vx, float* vy,
-                         float* life, uint64_t n, int threads) {
+                         uint64_t active_step, uint32_t clock, float* x, float* y, float* vx,
+                         float* vy, uint16_t* exp, uint64_t n, int threads) {
   step_consts k;
   make_consts(cfg, ext, active_step, &k);
-  if (!life) k.lifetime = 0;
+  k.clock = clock;
+  if (!exp) k.lifetime = 0;
 #ifdef _OPENMP
   if (threads > 0) omp_set_num_threads(threads);
 #pragma omp parallel for schedule(static)
 #endif
   for (int64_t i = 0; i < (int64_t)n; ++i) {
     stream_one(cfg, ext, &k, id_offset + (uint64_t)i, &x[i], &y[i], &vx[i], &vy[i],
-               k.lifetime ? &life[i] : NULL);
+               k.lifetime ? &exp[i] : NULL);
   }
   (void)threads;
 }
@@ -328,8 +345,8 @@ void orc_stream_step_omp(const rps_config* cfg, const rps_ext_config* ext, uint6
 /* Restatement of setup_particles_scatter (src/main.rs:182-216) with a seeded Philox stream
  * in place of the unseeded rand::rng() (src/main.rs:188). */
 void orc_init_scatter(const rps_config* cfg, const rps_ext_config* ext, uint64_t seed,
-                      uint64_t id_offset, uint64_t global_count, float* x, float* y,
-                      float* vx, float* vy, float* life, uint64_t n) {
+                      uint64_t id_offset, uint64_t global_count, uint32_t clock, float* x,
+                      float* y, float* vx, float* vy, uint16_t* exp, uint64_t n) {
   const float x_min = cfg->screen_bounds[0], x_max = cfg->screen_bounds[1];
   const float y_min = cfg->screen_bounds[2], y_max = cfg->screen_bounds[3];
   const float y_center = (y_min + y_max) / 2.0f;
@@ -353,7 +370,11 @@ void orc_init_scatter(const rps_config* cfg, const rps_ext_config* ext, uint64_t
     y[i] = yy;
     vx[i] = 0.0f;
     vy[i] = 0.0f;
-    if (life) life[i] = ext->life_min + u01(w[2]) * (ext->life_max - ext->life_min);
+    if (exp)
+      exp[i] = (uint16_t)(clock +
+                          orc_life_steps(ext->life_min + u01(w[2]) * (ext->life_max - ext->life_min),
+                                         cfg->fixed_delta_time) -
+                          1u);
   }
 }
 

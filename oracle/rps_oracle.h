@@ -46,20 +46,28 @@ uint32_t orc_cell_key(int32_t cx, int32_t cy, uint32_t n);
 /* WGSL i32(f32): truncate toward zero, saturate, NaN -> 0. */
 int32_t orc_f32_to_i32(float v);
 
-/* One active stream step (mode STREAM) over n particles with global ids id_offset+i.
- * life may be NULL when RPS_EXT_LIFETIME is off.  stats may be NULL. */
+/* Lifetime (build-defined): a particle keeps a u16 expiry e = the lifetime-
+ * clock value of the step in which it respawns; L seconds last clamp(ceil(L/dt), 1, 65535)
+ * steps.  Conversions at lifetime clock c (the clock of the next step). */
+uint32_t orc_life_steps(float life, float dt);
+void orc_exp_from_life(const float* life, uint64_t n, uint32_t clock, float dt, uint16_t* exp);
+void orc_life_from_exp(const uint16_t* exp, uint64_t n, uint32_t clock, float dt, float* life);
+
+/* One active stream step (mode STREAM) over n particles with global ids id_offset+i;
+ * active_step keys the Philox respawn stream, clock is this step's lifetime clock.
+ * exp may be NULL when RPS_EXT_LIFETIME is off.  stats may be NULL. */
 void orc_stream_step(const rps_config* cfg, const rps_ext_config* ext, uint64_t id_offset,
-                     uint64_t active_step, float* x, float* y, float* vx, float* vy,
-                     float* life, uint64_t n, orc_stats* stats);
+                     uint64_t active_step, uint32_t clock, float* x, float* y, float* vx,
+                     float* vy, uint16_t* exp, uint64_t n, orc_stats* stats);
 /* Same, OpenMP-parallel over particles (bench cpu_baseline); identical results. */
 void orc_stream_step_omp(const rps_config* cfg, const rps_ext_config* ext, uint64_t id_offset,
-                         uint64_t active_step, float* x, float* y, float* vx, float* vy,
-                         float* life, uint64_t n, int threads);
+                         uint64_t active_step, uint32_t clock, float* x, float* y, float* vx,
+                         float* vy, uint16_t* exp, uint64_t n, int threads);
 
-/* Device-init restatement (rps_init_scatter). */
+/* Device-init restatement (rps_init_scatter) at lifetime clock `clock`. */
 void orc_init_scatter(const rps_config* cfg, const rps_ext_config* ext, uint64_t seed,
-                      uint64_t id_offset, uint64_t global_count, float* x, float* y,
-                      float* vx, float* vy, float* life, uint64_t n);
+                      uint64_t id_offset, uint64_t global_count, uint32_t clock, float* x,
+                      float* y, float* vx, float* vy, uint16_t* exp, uint64_t n);
 
 /* All-pairs softened gravity: acc of targets [t0, t0+nt) from all ns sources. */
 void orc_nbody_accel(const rps_ext_config* ext, const float* sx, const float* sy, uint64_t ns,

@@ -36,8 +36,10 @@ struct rps_ctx {
   char* arena = nullptr;
   size_t arena_bytes = 0;
   Layout layout = plain_layout();  // tiled for STREAM (rps_device.hpp)
-  float* state = nullptr;          // STREAM: the tiled x|y|vx|vy|life block
-  float *x = nullptr, *y = nullptr, *vx = nullptr, *vy = nullptr, *life = nullptr;
+  Layout exp_layout = plain_layout();
+  float* state = nullptr;          // STREAM: the tiled x|y|vx|vy|expiry block
+  float *x = nullptr, *y = nullptr, *vx = nullptr, *vy = nullptr;
+  uint16_t* exp = nullptr;         // STREAM: lifetime expiry (u16)
   // SPH
   float *vx2 = nullptr, *vy2 = nullptr, *x2 = nullptr, *y2 = nullptr;
   f2 *pred_s = nullptr, *vel_s = nullptr, *dens_s = nullptr;
@@ -67,6 +69,7 @@ struct rps_ctx {
   uint64_t staging_cap = 0;
   // counters
   uint64_t active_steps = 0;
+  uint64_t life_clock = 0;  // active steps run with RPS_EXT_LIFETIME on (the expiry clock)
   bool stepped = false;
   // profiling
   uint32_t profile_every = 0;  // 0: off; k: events around every k-th dominant launch
@@ -77,6 +80,7 @@ struct rps_ctx {
   // tuning
   uint32_t stream_grid = 0;  // 0: one-shot grid
   int nontemporal = 3;
+  uint32_t xcd_order = 0;
   // comm
   ncclComm_t comm = nullptr;
   int rank = 0, nranks = 1;
@@ -141,7 +145,7 @@ int check_ctx(rps_ctx* ctx) {
 }
 
 Fields fields(const rps_ctx* ctx) {
-  return Fields{ctx->x, ctx->y, ctx->vx, ctx->vy, ctx->life};
+  return Fields{ctx->x, ctx->y, ctx->vx, ctx->vy, ctx->exp};
 }
 
 float* field_ptr(rps_ctx* ctx, int field) {
@@ -150,7 +154,6 @@ float* field_ptr(rps_ctx* ctx, int field) {
     case RPS_FIELD_Y: return ctx->y;
     case RPS_FIELD_VX: return ctx->vx;
     case RPS_FIELD_VY: return ctx->vy;
-    case RPS_FIELD_LIFE: return ctx->life;
     default: return nullptr;
   }
 }
@@ -176,7 +179,8 @@ StreamArgs make_stream_args(const rps_ctx* ctx, uint64_t k) {
   a.y = ctx->y;
   a.vx = ctx->vx;
   a.vy = ctx->vy;
-  a.life = ctx->life;
+  a.exp = ctx->exp;
+  a.clock = (uint32_t)ctx->life_clock;
   a.partials = ctx->partials;
   a.n = ctx->n;
   a.id_offset = ctx->id_offset;
@@ -212,6 +216,7 @@ StreamArgs make_stream_args(const rps_ctx* ctx, uint64_t k) {
   a.key1 = (uint32_t)(e.seed >> 32);
   a.step_lo = (uint32_t)k;
   a.step_hi = (uint32_t)(k >> 32);
+  a.xcd_order = ctx->xcd_order;
   return a;
 }
 
@@ -297,11 +302,12 @@ int step_stream(rps_ctx* ctx) {
 
 // Temporal fusion (ext.fuse_steps > 1): `m` consecutive active steps starting at active-step
 // index k0 in one launch; `stats` reduces the state after the last of them.
-int step_stream_fused(rps_ctx* ctx, uint64_t k0, uint32_t m, bool stats) {
+int step_stream_fused(rps_ctx* ctx, uint64_t k0, uint32_t m, bool stats, uint64_t clock0) {
   const rps_ext_config& e = ctx->ext;
   FusedArgs fa;
   std::memset(&fa, 0, sizeof(fa));
   fa.base = make_stream_args(ctx, k0);
+  fa.base.clock = (uint32_t)clock0;
   fa.nsub = m;
   const double dt = (double)ctx->cfg.fixed_delta_time;
   for (uint32_t sub = 0; sub < m; ++sub)
@@ -461,6 +467,7 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
   ctx->ext = default_ext();
   ctx->stream_grid = (uint32_t)std::max(0, env_int("RPS_STREAM_GRID", 0));
   ctx->nontemporal = env_int("RPS_STREAM_NT", 3) & 3;  // bit 0 loads, bit 1 stores
+  ctx->xcd_order = env_int("RPS_STREAM_XCD", 0) != 0;  // measured slower
 
   auto bail = [&](int code) {
     std::string m = ctx->err;
@@ -484,9 +491,9 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
   struct Slot { void** p; size_t bytes; };
   std::vector<Slot> slots;
   if (ctx->mode == RPS_MODE_STREAM) {
-    // Tiled SoA: ceil(n / kTile) tiles of kFields x kTile floats (rps_device.hpp).
+    // Tiled SoA: ceil(n / kTile) tiles of 4 f32 + 1 u16 segments (rps_device.hpp).
     const size_t tiles = (n + kTile - 1) / kTile;
-    slots.push_back({(void**)&ctx->state, tiles * kFields * kTile * sizeof(float)});
+    slots.push_back({(void**)&ctx->state, tiles * kTileBytes});
   } else {
     slots.push_back({(void**)&ctx->x, nf});
     slots.push_back({(void**)&ctx->y, nf});
@@ -536,7 +543,8 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     ctx->y = ctx->state + kTile;
     ctx->vx = ctx->state + 2 * kTile;
     ctx->vy = ctx->state + 3 * kTile;
-    ctx->life = ctx->state + 4 * kTile;
+    ctx->exp = reinterpret_cast<uint16_t*>(ctx->state + 4 * kTile);
+    ctx->exp_layout = tiled_exp_layout();
   }
   // wgpu buffers are zero-initialised; the SPH lookup pad entries rely on it.
   if (hipMemsetAsync(ctx->arena, 0, ctx->arena_bytes, ctx->stream) != hipSuccess) {
@@ -678,20 +686,23 @@ int rps_export_particles(rps_ctx* ctx, rps_particle* device_dst, uint64_t offset
   return RPS_OK;
 }
 
+// RPS_FIELD_LIFE is not stored: it is derived from / converted to the u16 expiry at the
+// current lifetime clock, through the staging buffer.
 int rps_upload_field(rps_ctx* ctx, int field, const float* src, uint64_t offset, uint64_t n) {
   int rc = check_ctx(ctx);
   if (rc) return rc;
-  float* p = field_ptr(ctx, field);
-  if (!p) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "field not present in this mode");
+  const bool life = field == RPS_FIELD_LIFE || field == RPS_FIELD_LIFE_STEPS;
+  float* p = life ? nullptr : field_ptr(ctx, field);
+  if (life ? !ctx->exp : !p) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "field not present in this mode");
   if (!src && n) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "null source");
   if (offset + n > ctx->n) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "range exceeds particle_count");
   if (n == 0) return RPS_OK;
-  if (ctx->layout.mask == plain_layout().mask) {
+  if (!life && ctx->layout.mask == plain_layout().mask) {
     RPS_HIP(ctx, hipMemcpyAsync(p + offset, src, n * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
     RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return RPS_OK;
   }
-  // Tiled layout: dense chunk -> staging -> scatter into the tiles.
+  // Dense chunk -> staging -> scatter into the tiles (or convert into expiries).
   const uint64_t chunk = std::min<uint64_t>(n, kStagingChunk * (sizeof(rps_particle) / sizeof(float)));
   rc = ensure_staging(ctx, (chunk * sizeof(float) + sizeof(rps_particle) - 1) / sizeof(rps_particle));
   if (rc) return rc;
@@ -699,7 +710,12 @@ int rps_upload_field(rps_ctx* ctx, int field, const float* src, uint64_t offset,
   for (uint64_t done = 0; done < n; done += chunk) {
     const uint64_t m = std::min(chunk, n - done);
     RPS_HIP(ctx, hipMemcpyAsync(stage, src + done, m * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
-    RPS_HIP(ctx, launch_field_scatter(p, ctx->layout, offset + done, stage, m, ctx->stream));
+    if (life)
+      RPS_HIP(ctx, launch_life_scatter(ctx->exp, ctx->exp_layout, offset + done, stage, m,
+                                       (uint32_t)ctx->life_clock, ctx->cfg.fixed_delta_time,
+                                       field == RPS_FIELD_LIFE ? 0 : 2, ctx->stream));
+    else
+      RPS_HIP(ctx, launch_field_scatter(p, ctx->layout, offset + done, stage, m, ctx->stream));
     RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
   }
   return RPS_OK;
@@ -708,12 +724,13 @@ int rps_upload_field(rps_ctx* ctx, int field, const float* src, uint64_t offset,
 int rps_download_field(rps_ctx* ctx, int field, float* dst, uint64_t offset, uint64_t n) {
   int rc = check_ctx(ctx);
   if (rc) return rc;
-  float* p = field_ptr(ctx, field);
-  if (!p) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "field not present in this mode");
+  const bool life = field == RPS_FIELD_LIFE || field == RPS_FIELD_LIFE_STEPS;
+  float* p = life ? nullptr : field_ptr(ctx, field);
+  if (life ? !ctx->exp : !p) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "field not present in this mode");
   if (!dst && n) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "null destination");
   if (offset + n > ctx->n) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "range exceeds particle_count");
   if (n == 0) return RPS_OK;
-  if (ctx->layout.mask == plain_layout().mask) {
+  if (!life && ctx->layout.mask == plain_layout().mask) {
     RPS_HIP(ctx, hipMemcpyAsync(dst, p + offset, n * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
     RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return RPS_OK;
@@ -724,7 +741,12 @@ int rps_download_field(rps_ctx* ctx, int field, float* dst, uint64_t offset, uin
   float* stage = reinterpret_cast<float*>(ctx->d_staging);
   for (uint64_t done = 0; done < n; done += chunk) {
     const uint64_t m = std::min(chunk, n - done);
-    RPS_HIP(ctx, launch_field_gather(p, ctx->layout, offset + done, stage, m, ctx->stream));
+    if (life)
+      RPS_HIP(ctx, launch_life_gather(ctx->exp, ctx->exp_layout, offset + done, stage, m,
+                                      (uint32_t)ctx->life_clock, ctx->cfg.fixed_delta_time,
+                                      field == RPS_FIELD_LIFE ? 0 : 2, ctx->stream));
+    else
+      RPS_HIP(ctx, launch_field_gather(p, ctx->layout, offset + done, stage, m, ctx->stream));
     RPS_HIP(ctx, hipMemcpyAsync(dst + done, stage, m * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
     RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
   }
@@ -744,11 +766,27 @@ int rps_read_debug(rps_ctx* ctx, int which, void* dst, uint64_t bytes) {
     case RPS_DEBUG_PREDICTED: src = ctx->pred; want = ctx->n * 8; break;
     case RPS_DEBUG_ACCEL_X: src = ctx->ax; want = ctx->n * 4; break;
     case RPS_DEBUG_ACCEL_Y: src = ctx->ay; want = ctx->n * 4; break;
+    case RPS_DEBUG_EXPIRY: src = ctx->exp; want = ctx->n * 2; break;
     default: return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "unknown debug buffer");
   }
   if (!src) return fail(ctx, RPS_ERR_UNSUPPORTED, "debug buffer not present in this mode");
   if (bytes != want)
     return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "bytes must equal the buffer size (" + std::to_string(want) + ")");
+  if (which == RPS_DEBUG_EXPIRY) {  // tiled u16 -> dense, through the staging buffer
+    const uint64_t chunk = kStagingChunk * (sizeof(rps_particle) / sizeof(uint16_t));
+    rc = ensure_staging(ctx, kStagingChunk);
+    if (rc) return rc;
+    for (uint64_t done = 0; done < ctx->n; done += chunk) {
+      const uint64_t m = std::min(chunk, ctx->n - done);
+      RPS_HIP(ctx, launch_life_gather(ctx->exp, ctx->exp_layout, done,
+                                      reinterpret_cast<float*>(ctx->d_staging), m, 0, 0.0f, 1,
+                                      ctx->stream));
+      RPS_HIP(ctx, hipMemcpyAsync(static_cast<uint16_t*>(dst) + done, ctx->d_staging,
+                                  m * sizeof(uint16_t), hipMemcpyDeviceToHost, ctx->stream));
+      RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    return RPS_OK;
+  }
   RPS_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
   RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return RPS_OK;
@@ -770,6 +808,9 @@ int rps_init_scatter(rps_ctx* ctx, uint64_t seed) {
   a.global_count_f = (float)ctx->global_count;
   a.life_min = ctx->ext.life_min;
   a.life_range = ctx->ext.life_max - ctx->ext.life_min;
+  a.exp_layout = ctx->exp_layout;
+  a.clock = (uint32_t)ctx->life_clock;
+  a.dt = ctx->cfg.fixed_delta_time;
   a.key0 = (uint32_t)seed;
   a.key1 = (uint32_t)(seed >> 32);
   RPS_HIP(ctx, launch_init_scatter(a, ctx->stream));
@@ -788,7 +829,8 @@ int rps_step(rps_ctx* ctx, uint32_t nsteps) {
   const bool fused = ctx->mode == RPS_MODE_STREAM && fuse > 1;
   const uint32_t interval = std::max<uint32_t>(ctx->ext.stats_interval, 1u);
   uint32_t pending = 0;  // fused mode: active steps accumulated since the last launch
-  uint64_t pending_k0 = 0;
+  uint64_t pending_k0 = 0, pending_clock0 = 0;
+  const bool lifetime = (ctx->ext.flags & RPS_EXT_LIFETIME) != 0;
   for (uint32_t s = 0; s < nsteps; ++s) {
     ctx->cfg.frame_count += 1;  // src/particle_buffers.rs:227
     const bool active = ctx->cfg.frame_count >= ctx->ext.shader_delay;  // wgsl:426, :442
@@ -799,13 +841,17 @@ int rps_step(rps_ctx* ctx, uint32_t nsteps) {
     if (!active) continue;
     if (fused) {
       const uint64_t k = ctx->active_steps;
-      if (pending == 0) pending_k0 = k;
+      if (pending == 0) {
+        pending_k0 = k;
+        pending_clock0 = ctx->life_clock;
+      }
       ++pending;
       ++ctx->active_steps;
+      if (lifetime) ++ctx->life_clock;
       ctx->stepped = true;
       const bool stats = (ctx->ext.flags & RPS_EXT_STATS) && (k % interval == 0);
       if (pending == fuse || stats || s + 1 == nsteps) {
-        rc = step_stream_fused(ctx, pending_k0, pending, stats);
+        rc = step_stream_fused(ctx, pending_k0, pending, stats, pending_clock0);
         if (rc) return rc;
         pending = 0;
       }
@@ -818,9 +864,10 @@ int rps_step(rps_ctx* ctx, uint32_t nsteps) {
     }
     if (rc) return rc;
     ++ctx->active_steps;
+    if (lifetime && ctx->mode == RPS_MODE_STREAM) ++ctx->life_clock;
     ctx->stepped = true;
   }
-  if (pending) return step_stream_fused(ctx, pending_k0, pending, false);
+  if (pending) return step_stream_fused(ctx, pending_k0, pending, false, pending_clock0);
   return RPS_OK;
 }
 
@@ -908,8 +955,8 @@ int rps_step_cost(const rps_ctx* ctx, double* amount, int* unit) {
   if (!ctx || !amount || !unit) return fail(nullptr, RPS_ERR_INVALID_ARGUMENT, "null argument");
   switch (ctx->mode) {
     case RPS_MODE_STREAM: {
-      // r+w of x, y, vx, vy (+ life): DESIGN.md §5.
-      const double per = (ctx->ext.flags & RPS_EXT_LIFETIME) ? 40.0 : 32.0;
+      // r+w of x, y, vx, vy (+ the u16 expiry read): DESIGN.md §5.
+      const double per = (ctx->ext.flags & RPS_EXT_LIFETIME) ? 34.0 : 32.0;
       *amount = per * (double)ctx->n;
       *unit = 0;
       return RPS_OK;

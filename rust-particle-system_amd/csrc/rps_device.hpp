@@ -18,40 +18,57 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 constexpr int kMaxAttractors = 8;
 
 // Particle-state layout in HBM.  STREAM mode keeps the state as *tiled SoA*
-// (AoSoA): tiles of kTile particles, each tile holding kFields contiguous segments
-// [x | y | vx | vy | life] of kTile floats.  Lanes still read 16 contiguous bytes and a
-// wave 1 KiB of one field, but a workgroup's five streams fall in one 160 KiB region instead
-// of five arrays gigabytes apart: measured 6.35 TB/s vs 5.33 TB/s for plain SoA on the same
-// in-place 5-field update (tools/hbm_probe.hip).  SPH and N-body keep plain SoA.
+// (AoSoA): tiles of kTile particles, each tile holding four contiguous f32 segments
+// [x | y | vx | vy] followed by one u16 segment [expiry] (kTile * 18 B = 144 KiB).  Lanes
+// read 16 contiguous bytes (8 for the expiry) and a wave 1 KiB of one field, and a
+// workgroup's streams fall in one 144 KiB region instead of arrays gigabytes apart
+// (tools/hbm_probe.hip: 6.35-6.39 TB/s tiled vs 5.3 TB/s plain SoA on the in-place update).
+// SPH and N-body keep plain SoA.
 constexpr uint32_t kTileLog = 13;
 constexpr uint64_t kTile = 1ull << kTileLog;
-constexpr uint32_t kFields = 5;
+constexpr uint64_t kTileBytes = kTile * 18;  // 4 x f32 + 1 x u16 per particle
 
-// Element offset of particle i inside one field: (i & ~mask) * mult + (i & mask).
-// plain: mask = ~0 (offset i); tiled: mask = kTile-1, mult = kFields.
+// Element offset of particle i inside one field: (((i & ~mask) * mult) >> shift) + (i & mask).
+// plain: mask = ~0 (offset i).  Tiled f32 fields: the tile stride is 4.5 * kTile floats
+// (mult 9, shift 1); the tiled u16 expiry: 9 * kTile u16 (mult 9, shift 0).
 struct Layout {
   uint64_t mask;
   uint64_t mult;
+  uint32_t shift;
 };
 __host__ __device__ __forceinline__ uint64_t lidx(Layout L, uint64_t i) {
-  return (i & ~L.mask) * L.mult + (i & L.mask);
+  return (((i & ~L.mask) * L.mult) >> L.shift) + (i & L.mask);
 }
-__host__ __device__ __forceinline__ Layout plain_layout() { return Layout{~0ull, 1}; }
-__host__ __device__ __forceinline__ Layout tiled_layout() { return Layout{kTile - 1, kFields}; }
-// Tiled offset with compile-time constants (the stream kernel's address math).
+__host__ __device__ __forceinline__ Layout plain_layout() { return Layout{~0ull, 1, 0}; }
+__host__ __device__ __forceinline__ Layout tiled_layout() { return Layout{kTile - 1, 9, 1}; }
+__host__ __device__ __forceinline__ Layout tiled_exp_layout() { return Layout{kTile - 1, 9, 0}; }
+// Tiled offsets with compile-time constants (the stream kernel's address math).
 __device__ __forceinline__ uint64_t tidx(uint64_t i) {
-  return (i & ~(kTile - 1)) * kFields + (i & (kTile - 1));
+  return (((i & ~(kTile - 1)) * 9) >> 1) + (i & (kTile - 1));
+}
+__device__ __forceinline__ uint64_t eidx(uint64_t i) {
+  return (i & ~(kTile - 1)) * 9 + (i & (kTile - 1));
 }
 
-// Base pointers of the (up to) five fields; for the tiled layout field f starts at
-// tile-0 offset f * kTile.
+// Base pointers of the fields; for the tiled layout f32 field f starts at tile-0 offset
+// f * kTile floats and the expiry at byte 4 * kTile * 4.
 struct Fields {
   float* x;
   float* y;
   float* vx;
   float* vy;
-  float* life;  // may be null
+  uint16_t* exp;  // lifetime expiry (STREAM only; may be null)
 };
+
+// Lifetime in whole steps: a lifetime of L seconds lasts
+// clamp(ceil(L / dt), 1, 65535) active lifetime steps.  f32 division, correctly rounded on
+// both sides (oracle: orc_life_steps).
+__host__ __device__ __forceinline__ uint32_t life_steps(float life, float dt) {
+  const float q = ceilf(life / dt);
+  if (!(q >= 1.0f)) return 1u;
+  if (q >= 65535.0f) return 65535u;
+  return (uint32_t)q;
+}
 
 // Per-step uniforms of the streaming kernel.  Passed by value: the kernarg segment lands in
 // SGPRs through s_load, so the 4-8 attractors cost no LDS and no VGPRs.
@@ -60,7 +77,7 @@ struct StreamArgs {
   float* __restrict__ y;
   float* __restrict__ vx;
   float* __restrict__ vy;
-  float* __restrict__ life;
+  uint16_t* __restrict__ exp;  // lifetime expiry, tiled u16 (eidx)
   struct StatsPartial* partials;  // one per workgroup when stats are on
   uint64_t n;                     // particles in this shard
   uint64_t id_offset;             // global id of particle 0
@@ -71,6 +88,8 @@ struct StreamArgs {
   float x_min, x_max, y_min, y_max, damping;
   float emit_cx, emit_cy, emit_r, spd_min, spd_range, life_min, life_range;
   uint32_t key0, key1, step_lo, step_hi;
+  uint32_t clock;      // lifetime clock of this step (low 16 bits compared with the expiry)
+  uint32_t xcd_order;  // 1: workgroup b takes block xcd_block(b) (contiguous range per XCD)
 };
 
 // Temporal fusion of up to kMaxFuse consecutive active steps in one launch: per-substep
@@ -236,8 +255,9 @@ __device__ __forceinline__ void attract(const StreamArgs& a, const float* apx, c
   ay = sy;
 }
 
-__device__ __forceinline__ void respawn(const StreamArgs& a, uint64_t step, uint64_t gid, float& x,
-                                        float& y, float& vx, float& vy, float& life) {
+// Respawn at the emitter; returns the new lifetime in steps.
+__device__ __forceinline__ uint32_t respawn(const StreamArgs& a, uint64_t step, uint64_t gid,
+                                            float& x, float& y, float& vx, float& vy) {
   uint32_t w[4];
   philox4x32_10((uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)step, (uint32_t)(step >> 32), a.key0,
                 a.key1, w);
@@ -249,15 +269,17 @@ __device__ __forceinline__ void respawn(const StreamArgs& a, uint64_t step, uint
   const float spd = a.spd_min + u01(w[3]) * a.spd_range;
   vx = spd * c;
   vy = spd * s;
-  life = a.life_min + u01(w[2]) * a.life_range;
+  return life_steps(a.life_min + u01(w[2]) * a.life_range, a.dt);
 }
 
 // One particle, one active step.  Returns true when the particle respawned.
-// (apx, apy): attractor positions of this step; step: its active-step index (Philox counter).
+// (apx, apy): attractor positions of this step; step: its active-step index (Philox counter);
+// clock: its lifetime-clock value; e: the particle's expiry (the clock value of the step in
+// which it respawns, mod 2^16).
 template <bool VERLET, bool LIFETIME>
 __device__ __forceinline__ bool step_one(const StreamArgs& a, const float* apx, const float* apy,
-                                         uint64_t step, uint64_t gid, float& x, float& y,
-                                         float& vx, float& vy, float& life) {
+                                         uint64_t step, uint32_t clock, uint64_t gid, float& x,
+                                         float& y, float& vx, float& vy, uint16_t& e) {
   const float dt = a.dt;
   if constexpr (!VERLET) {
     vx = vx + a.gx_dt;  // apply_gravity, wgsl:397-400
@@ -293,9 +315,8 @@ __device__ __forceinline__ bool step_one(const StreamArgs& a, const float* apx, 
   }
   wall(a.x_min, a.x_max, a.y_min, a.y_max, a.damping, x, y, vx, vy);
   if constexpr (LIFETIME) {
-    life = life - dt;
-    if (life <= 0.0f) {
-      respawn(a, step, gid, x, y, vx, vy, life);
+    if (e == (uint16_t)clock) {
+      e = (uint16_t)(clock + respawn(a, step, gid, x, y, vx, vy));
       return true;
     }
   }

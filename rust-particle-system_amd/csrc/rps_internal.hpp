@@ -37,10 +37,18 @@ hipError_t launch_field_gather(const float* field, Layout L, uint64_t offset, fl
                                uint64_t n, hipStream_t s);
 hipError_t launch_field_scatter(float* field, Layout L, uint64_t offset, const float* in,
                                 uint64_t n, hipStream_t s);
+// Lifetime expiry <-> its views at lifetime clock `clock`; mode 0 seconds, 1 raw u16
+// (gather only), 2 steps left (kernels: life_gather/scatter_kernel).
+hipError_t launch_life_gather(const uint16_t* exp, Layout L, uint64_t offset, float* out,
+                              uint64_t n, uint32_t clock, float dt, int mode, hipStream_t s);
+hipError_t launch_life_scatter(uint16_t* exp, Layout L, uint64_t offset, const float* in,
+                               uint64_t n, uint32_t clock, float dt, int mode, hipStream_t s);
 
 struct InitArgs {
-  Fields f;  // life may be null
-  Layout layout;
+  Fields f;  // exp may be null
+  Layout layout, exp_layout;
+  uint32_t clock;
+  float dt;
   uint64_t n, id_offset;
   float x_min, x_max, y_min, y_max, global_count_f, life_min, life_range;
   uint32_t key0, key1;

@@ -31,6 +31,25 @@ __device__ __forceinline__ void st4(float* p, f4 v) {
   }
 }
 
+// Four u16 expiries (8 B per lane, 512 B per wave).
+typedef uint16_t h4 __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ h4 lde4(const uint16_t* p) {
+  if constexpr (NT) {
+    return __builtin_nontemporal_load(reinterpret_cast<const h4*>(p));
+  } else {
+    return *reinterpret_cast<const h4*>(p);
+  }
+}
+template <bool NT>
+__device__ __forceinline__ void ste4(uint16_t* p, h4 v) {
+  if constexpr (NT) {
+    __builtin_nontemporal_store(v, reinterpret_cast<h4*>(p));
+  } else {
+    *reinterpret_cast<h4*>(p) = v;
+  }
+}
+
 struct StatsAcc {
   float x0, x1, y0, y1;
   double ke;
@@ -96,17 +115,28 @@ __device__ void block_reduce_stats(StatsAcc acc, StatsPartial* out) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Streaming step: one fused pass per active step.  SoA x|y|vx|vy[|life] read and written
-// in place with 16-B vector accesses (4 particles per lane), grid-stride.  40 B/particle
-// with lifetime, 32 B without.
+// Streaming step: one fused pass per active step.  SoA x|y|vx|vy read and written
+// in place with 16-B vector accesses (4 particles per lane), grid-stride.  32 B/particle
+// of x, y, vx, vy read+write; with lifetime +2 B of expiry read (written only by the lanes
+// whose particles respawn), 34 B/particle.
 // ---------------------------------------------------------------------------------------
 // NTM: bit 0 = nontemporal loads, bit 1 = nontemporal stores.
+// Workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, "Workgroup
+// dispatch"): with xcd_order, workgroup b takes block x*q + min(x, r) + b/8 (x = b % 8,
+// q = G/8, r = G%8), a bijection that gives each XCD one contiguous range of tiles.
+// Speed only; every particle is still visited exactly once.
+__device__ __forceinline__ uint64_t stream_block(const StreamArgs& a, uint32_t b) {
+  if (!a.xcd_order) return b;
+  const uint32_t G = gridDim.x, q = G / 8, r = G % 8, x = b % 8, k = b / 8;
+  return (uint64_t)x * q + (x < r ? x : r) + k;
+}
+
 template <bool VERLET, bool LIFETIME, bool STATS, int NTM>
 __global__ __launch_bounds__(kBlock) void stream_step_kernel(StreamArgs a) {
   constexpr bool NTL = (NTM & 1) != 0, NTS = (NTM & 2) != 0;
   const uint64_t nvec = a.n >> 2;
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-  const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint64_t tid = stream_block(a, blockIdx.x) * kBlock + threadIdx.x;
   const uint64_t step = ((uint64_t)a.step_hi << 32) | a.step_lo;
   StatsAcc acc;
   if constexpr (STATS) acc.init();
@@ -117,25 +147,30 @@ __global__ __launch_bounds__(kBlock) void stream_step_kernel(StreamArgs a) {
     f4 Y = ld4<NTL>(a.y + o);
     f4 VX = ld4<NTL>(a.vx + o);
     f4 VY = ld4<NTL>(a.vy + o);
-    f4 L = {0.0f, 0.0f, 0.0f, 0.0f};
-    if constexpr (LIFETIME) L = ld4<NTL>(a.life + o);
+    h4 E = {0, 0, 0, 0};
+    if constexpr (LIFETIME) E = lde4<NTL>(a.exp + eidx(i));
+    bool any = false;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      float x = X[c], y = Y[c], vx = VX[c], vy = VY[c], life = L[c];
-      const bool re = step_one<VERLET, LIFETIME>(a, a.ax, a.ay, step, a.id_offset + i + c, x, y, vx,
-                                                 vy, life);
+      float x = X[c], y = Y[c], vx = VX[c], vy = VY[c];
+      uint16_t e = E[c];
+      const bool re = step_one<VERLET, LIFETIME>(a, a.ax, a.ay, step, a.clock, a.id_offset + i + c, x,
+                                                 y, vx, vy, e);
       X[c] = x;
       Y[c] = y;
       VX[c] = vx;
       VY[c] = vy;
-      L[c] = life;
+      E[c] = e;
+      any |= re;
       if constexpr (STATS) acc.add(x, y, vx, vy, re);
     }
     st4<NTS>(a.x + o, X);
     st4<NTS>(a.y + o, Y);
     st4<NTS>(a.vx + o, VX);
     st4<NTS>(a.vy + o, VY);
-    if constexpr (LIFETIME) st4<NTS>(a.life + o, L);
+    if constexpr (LIFETIME) {
+      if (any) ste4<NTS>(a.exp + eidx(i), E);  // expiry written only on respawn
+    }
   }
   // n % 4 tail particles, one per lane of the first threads.
   const uint64_t rem = a.n - (nvec << 2);
@@ -143,14 +178,16 @@ __global__ __launch_bounds__(kBlock) void stream_step_kernel(StreamArgs a) {
     const uint64_t i = (nvec << 2) + tid;
     const uint64_t o = tidx(i);
     float x = a.x[o], y = a.y[o], vx = a.vx[o], vy = a.vy[o];
-    float life = LIFETIME ? a.life[o] : 0.0f;
-    const bool re = step_one<VERLET, LIFETIME>(a, a.ax, a.ay, step, a.id_offset + i, x, y, vx, vy,
-                                               life);
+    uint16_t e = LIFETIME ? a.exp[eidx(i)] : 0;
+    const bool re = step_one<VERLET, LIFETIME>(a, a.ax, a.ay, step, a.clock, a.id_offset + i, x, y, vx,
+                                               vy, e);
     a.x[o] = x;
     a.y[o] = y;
     a.vx[o] = vx;
     a.vy[o] = vy;
-    if constexpr (LIFETIME) a.life[o] = life;
+    if constexpr (LIFETIME) {
+      if (re) a.exp[eidx(i)] = e;
+    }
     if constexpr (STATS) acc.add(x, y, vx, vy, re);
   }
   if constexpr (STATS) block_reduce_stats(acc, a.partials);
@@ -165,7 +202,7 @@ __global__ __launch_bounds__(kBlock) void stream_fused_kernel(FusedArgs fa) {
   const StreamArgs& a = fa.base;
   const uint64_t nvec = a.n >> 2;
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-  const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint64_t tid = stream_block(a, blockIdx.x) * kBlock + threadIdx.x;
   const uint64_t step0 = ((uint64_t)a.step_hi << 32) | a.step_lo;
   StatsAcc acc;
   if constexpr (STATS) acc.init();
@@ -176,20 +213,23 @@ __global__ __launch_bounds__(kBlock) void stream_fused_kernel(FusedArgs fa) {
     f4 Y = ld4<NTL>(a.y + o);
     f4 VX = ld4<NTL>(a.vx + o);
     f4 VY = ld4<NTL>(a.vy + o);
-    f4 L = {0.0f, 0.0f, 0.0f, 0.0f};
-    if constexpr (LIFETIME) L = ld4<NTL>(a.life + o);
+    h4 E = {0, 0, 0, 0};
+    if constexpr (LIFETIME) E = lde4<NTL>(a.exp + eidx(i));
     bool re[4] = {false, false, false, false};
+    bool any = false;
     for (uint32_t sub = 0; sub < fa.nsub; ++sub) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        float x = X[c], y = Y[c], vx = VX[c], vy = VY[c], life = L[c];
-        re[c] = step_one<VERLET, LIFETIME>(a, fa.ax[sub], fa.ay[sub], step0 + sub, a.id_offset + i + c,
-                                           x, y, vx, vy, life);
+        float x = X[c], y = Y[c], vx = VX[c], vy = VY[c];
+        uint16_t e = E[c];
+        re[c] = step_one<VERLET, LIFETIME>(a, fa.ax[sub], fa.ay[sub], step0 + sub, a.clock + sub,
+                                           a.id_offset + i + c, x, y, vx, vy, e);
         X[c] = x;
         Y[c] = y;
         VX[c] = vx;
         VY[c] = vy;
-        L[c] = life;
+        E[c] = e;
+        any |= re[c];
       }
     }
     if constexpr (STATS) {
@@ -200,23 +240,29 @@ __global__ __launch_bounds__(kBlock) void stream_fused_kernel(FusedArgs fa) {
     st4<NTS>(a.y + o, Y);
     st4<NTS>(a.vx + o, VX);
     st4<NTS>(a.vy + o, VY);
-    if constexpr (LIFETIME) st4<NTS>(a.life + o, L);
+    if constexpr (LIFETIME) {
+      if (any) ste4<NTS>(a.exp + eidx(i), E);
+    }
   }
   const uint64_t rem = a.n - (nvec << 2);
   if (tid < rem) {
     const uint64_t i = (nvec << 2) + tid;
     const uint64_t o = tidx(i);
     float x = a.x[o], y = a.y[o], vx = a.vx[o], vy = a.vy[o];
-    float life = LIFETIME ? a.life[o] : 0.0f;
-    bool re = false;
-    for (uint32_t sub = 0; sub < fa.nsub; ++sub)
-      re = step_one<VERLET, LIFETIME>(a, fa.ax[sub], fa.ay[sub], step0 + sub, a.id_offset + i, x, y, vx,
-                                      vy, life);
+    uint16_t e = LIFETIME ? a.exp[eidx(i)] : 0;
+    bool re = false, any = false;
+    for (uint32_t sub = 0; sub < fa.nsub; ++sub) {
+      re = step_one<VERLET, LIFETIME>(a, fa.ax[sub], fa.ay[sub], step0 + sub, a.clock + sub,
+                                      a.id_offset + i, x, y, vx, vy, e);
+      any |= re;
+    }
     a.x[o] = x;
     a.y[o] = y;
     a.vx[o] = vx;
     a.vy[o] = vy;
-    if constexpr (LIFETIME) a.life[o] = life;
+    if constexpr (LIFETIME) {
+      if (any) a.exp[eidx(i)] = e;
+    }
     if constexpr (STATS) acc.add(x, y, vx, vy, re);
   }
   if constexpr (STATS) block_reduce_stats(acc, a.partials);
@@ -315,6 +361,34 @@ __global__ __launch_bounds__(kBlock) void field_scatter_kernel(float* field, Lay
   if (j < n) field[lidx(L, offset + j)] = in[j];
 }
 
+// Lifetime field views.  Before the step with lifetime clock c, a particle
+// with expiry e has (u16)(e - c) + 1 steps left.  mode 0: life in seconds = steps * dt;
+// mode 1: the raw u16 expiry (debug); mode 2: steps left as an exact f32 integer.  Writing
+// (life_scatter): mode 0 takes seconds, e = c + life_steps(L) - 1; mode 2 takes steps,
+// e = c + clamp(ceil(v), 1, 65535) - 1.
+__global__ __launch_bounds__(kBlock) void life_gather_kernel(const uint16_t* exp, Layout L,
+                                                             uint64_t offset, float* out, uint64_t n,
+                                                             uint32_t clock, float dt, int mode) {
+  const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j >= n) return;
+  const uint16_t e = exp[lidx(L, offset + j)];
+  const float left = (float)((uint32_t)(uint16_t)(e - (uint16_t)clock) + 1u);
+  if (mode == 1)
+    reinterpret_cast<uint16_t*>(out)[j] = e;
+  else
+    out[j] = mode == 2 ? left : left * dt;
+}
+
+__global__ __launch_bounds__(kBlock) void life_scatter_kernel(uint16_t* exp, Layout L,
+                                                              uint64_t offset, const float* in,
+                                                              uint64_t n, uint32_t clock, float dt,
+                                                              int mode) {
+  const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j >= n) return;
+  const uint32_t steps = mode == 2 ? life_steps(in[j], 1.0f) : life_steps(in[j], dt);
+  exp[lidx(L, offset + j)] = (uint16_t)(clock + steps - 1u);
+}
+
 // ---------------------------------------------------------------------------------------
 // Initial scatter (seeded restatement of src/main.rs:182-216)
 // ---------------------------------------------------------------------------------------
@@ -339,7 +413,9 @@ __global__ __launch_bounds__(kBlock) void init_scatter_kernel(InitArgs a) {
   a.f.y[o] = yy;
   a.f.vx[o] = 0.0f;
   a.f.vy[o] = 0.0f;
-  if (a.f.life) a.f.life[o] = a.life_min + u01(w[2]) * a.life_range;
+  if (a.f.exp)
+    a.f.exp[lidx(a.exp_layout, i)] =
+        (uint16_t)(a.clock + life_steps(a.life_min + u01(w[2]) * a.life_range, a.dt) - 1u);
   }
 }
 
@@ -928,6 +1004,22 @@ hipError_t launch_field_gather(const float* field, Layout L, uint64_t offset, fl
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(field_gather_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, s, field, L, offset,
                      out, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_life_gather(const uint16_t* exp, Layout L, uint64_t offset, float* out,
+                              uint64_t n, uint32_t clock, float dt, int mode, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(life_gather_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, s, exp, L, offset,
+                     out, n, clock, dt, mode);
+  return hipGetLastError();
+}
+
+hipError_t launch_life_scatter(uint16_t* exp, Layout L, uint64_t offset, const float* in,
+                               uint64_t n, uint32_t clock, float dt, int mode, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(life_scatter_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, s, exp, L, offset,
+                     in, n, clock, dt, mode);
   return hipGetLastError();
 }
 

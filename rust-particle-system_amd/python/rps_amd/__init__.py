@@ -45,8 +45,10 @@ EULER, VERLET = 0, 1
 EXT_LIFETIME, EXT_STATS = 1, 2
 MAX_ATTRACTORS = 8
 FIELD_X, FIELD_Y, FIELD_VX, FIELD_VY, FIELD_LIFE = 0, 1, 2, 3, 4
+FIELD_LIFE_STEPS = 5  # whole lifetime steps left (exact); FIELD_LIFE = that * dt seconds
 DEBUG_SPATIAL_LOOKUP, DEBUG_LOOKUP_OFFSETS, DEBUG_DENSITIES, DEBUG_PREDICTED = 16, 17, 18, 19
 DEBUG_ACCEL_X, DEBUG_ACCEL_Y = 20, 21
+DEBUG_EXPIRY = 22  # u16 lifetime expiry per particle (STREAM)
 
 # Particle, src/particle.rs:20-25 (32 bytes: position @0, velocity @8, color @16)
 PARTICLE_DTYPE = np.dtype([("position", "<f4", (2,)), ("velocity", "<f4", (2,)), ("color", "<f4", (4,))])
@@ -454,6 +456,7 @@ class Context:
             DEBUG_PREDICTED: (np.float32, 2 * self.n),
             DEBUG_ACCEL_X: (np.float32, self.n),
             DEBUG_ACCEL_Y: (np.float32, self.n),
+            DEBUG_EXPIRY: (np.uint16, self.n),
         }[which]
         count = spec[1]
         if count is None:

@@ -104,8 +104,29 @@ def wall(bounds, damp, x, y, vx, vy):
     return x.astype(F), y.astype(F), vx.astype(F), vy.astype(F)
 
 
-def stream_step(cfg, ext, soa, active_step, id_offset=0):
-    """One active stream step; cfg/ext are plain dicts (see tests/test_oracle_semantics.py)."""
+def life_steps(life, dt):
+    """clamp(ceil(L / dt), 1, 65535) in f32, vectorised."""
+    with np.errstate(divide="ignore", invalid="ignore"):
+        q = np.ceil(np.asarray(life, F) / F(dt)).astype(F)
+    out = np.where(q >= F(65535.0), F(65535.0), q)
+    out = np.where(q >= F(1.0), out, F(1.0))  # NaN and q < 1 -> 1
+    return out.astype(np.uint32)
+
+
+def exp_from_life(life, clock, dt):
+    return ((np.uint32(clock & 0xFFFFFFFF) + life_steps(life, dt) - np.uint32(1)) & np.uint32(0xFFFF)).astype(np.uint16)
+
+
+def life_from_exp(exp, clock, dt):
+    left = (exp.astype(np.uint32) - np.uint32(clock & 0xFFFF)) & np.uint32(0xFFFF)
+    return ((left + np.uint32(1)).astype(F) * F(dt)).astype(F)
+
+
+def stream_step(cfg, ext, soa, active_step, id_offset=0, clock=None):
+    """One active stream step; cfg/ext are plain dicts (see tests/test_oracle_semantics.py).
+    clock: the step's lifetime clock (default active_step); soa["exp"] (u16) is the lifetime
+    state, created from soa["life"] at `clock` when absent."""
+    clock = active_step if clock is None else clock
     dt = F(cfg["dt"])
     g = F(cfg["gravity"])
     x, y, vx, vy = (soa[k].copy() for k in ("x", "y", "vx", "vy"))
@@ -142,8 +163,9 @@ def stream_step(cfg, ext, soa, active_step, id_offset=0):
     x, y, vx, vy = wall(cfg["bounds"], cfg["damping"], x, y, vx, vy)
     out = dict(x=x, y=y, vx=vx, vy=vy)
     if ext.get("lifetime"):
-        life = soa["life"] - dt
-        re = life <= F(0.0)
+        exp = soa.get("exp")
+        exp = exp_from_life(soa["life"], clock, dt) if exp is None else exp.copy()
+        re = exp == np.uint16(clock & 0xFFFF)
         idx = np.nonzero(re)[0]
         if len(idx):
             gid = np.uint64(id_offset) + idx.astype(np.uint64)
@@ -160,8 +182,10 @@ def stream_step(cfg, ext, soa, active_step, id_offset=0):
             vx[idx] = spd * c
             vy[idx] = spd * s
             lmin, lmax = F(ext["lifetime"][0]), F(ext["lifetime"][1])
-            life[idx] = lmin + u01(w[2]) * (lmax - lmin)
-        out["life"] = life.astype(F)
+            steps = life_steps(lmin + u01(w[2]) * (lmax - lmin), dt)
+            exp[idx] = ((np.uint32(clock & 0xFFFFFFFF) + steps) & np.uint32(0xFFFF)).astype(np.uint16)
+        out["exp"] = exp
+        out["life"] = life_from_exp(exp, clock + 1, dt)
     return out
 
 

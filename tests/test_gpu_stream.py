@@ -1,6 +1,6 @@
 """GPU parity of the streaming step (mode STREAM) against the CPU oracle, through the C ABI.
 
-Bar: bitwise for every field (x, y, vx, vy, life), every step — the kernels and the oracle
+Bar: bitwise for every field (x, y, vx, vy, life and the raw u16 expiry), every step — the kernels and the oracle
 both compute IEEE f32 with no contraction and correctly-rounded div/sqrt."""
 import numpy as np
 import pytest
@@ -11,6 +11,13 @@ from helpers import (F, assert_bitwise, assert_soa_bitwise, config_c1, copy_soa,
 pytestmark = pytest.mark.gpu
 
 KEYS5 = ("x", "y", "vx", "vy", "life")
+KEYS_STEPS = ("x", "y", "vx", "vy", "steps")
+
+
+def _download_chunk(rps, ctx, start, n):
+    """x, y, vx, vy and the exact lifetime steps left of particles [start, start+n)."""
+    fields = (rps.FIELD_X, rps.FIELD_Y, rps.FIELD_VX, rps.FIELD_VY, rps.FIELD_LIFE_STEPS)
+    return {k: ctx.download_field(f, start, n) for k, f in zip(KEYS_STEPS, fields)}
 
 
 def _gpu_ctx(rps, n, cfg, ext, soa, id_offset=0, global_count=0):
@@ -78,6 +85,7 @@ def test_headline_features_bitwise(gpu, orc):
             orc.stream_step(cfg, ext, ref, s)
         ctx.step(25)
         assert_soa_bitwise(ctx.download_soa(life=True), ref, keys=KEYS5)
+        assert_bitwise(ctx.read_debug(rps.DEBUG_EXPIRY), ref["exp"], "expiry")
 
 
 @pytest.mark.parametrize("n", [1, 3, 5, 63, 1023, 4097, 65539])
@@ -93,6 +101,7 @@ def test_ragged_sizes(gpu, orc, n):
             orc.stream_step(cfg, ext, ref, s)
         ctx.step(5)
         assert_soa_bitwise(ctx.download_soa(life=True), ref, keys=KEYS5)
+        assert_bitwise(ctx.read_debug(rps.DEBUG_EXPIRY), ref["exp"], "expiry")
 
 
 def test_sharded_contexts_use_global_ids(gpu, orc):
@@ -168,16 +177,17 @@ def test_full_size_sampled_parity(gpu, orc):
         ctx.init_scatter(seed=0x5EED)
         ctx.step(4)  # gated frames
         ctx.step(30)
-        fields = (rps.FIELD_X, rps.FIELD_Y, rps.FIELD_VX, rps.FIELD_VY, rps.FIELD_LIFE)
-        before = [{k: ctx.download_field(f, s, chunk) for k, f in zip(KEYS5, fields)} for s in starts]
+        before = [_download_chunk(rps, ctx, s, chunk) for s in starts]
         ctx.step(3)
         _, act = ctx.counters()
-        after = [{k: ctx.download_field(f, s, chunk) for k, f in zip(KEYS5, fields)} for s in starts]
+        after = [_download_chunk(rps, ctx, s, chunk) for s in starts]
     assert act == 33
     for s, b, a in zip(starts, before, after):
+        b["exp"] = orc.exp_from_steps(b.pop("steps"), 30)
         for k in range(30, 33):
             orc.stream_step(cfg, ext, b, k, id_offset=s)
-        assert_soa_bitwise(a, b, keys=KEYS5, what=f"chunk@{s} ")
+        b["steps"] = orc.steps_from_exp(b["exp"], 33)
+        assert_soa_bitwise(a, b, keys=KEYS_STEPS, what=f"chunk@{s} ")
 
 
 def test_aos_roundtrip_and_errors(gpu):
@@ -224,7 +234,7 @@ def test_profiling_counts_dominant_kernel(gpu):
         ms, cnt = ctx.kernel_time()
         assert cnt == 7 and ms > 0
         amt, unit = ctx.step_cost()
-        assert unit == "bytes" and amt == 40.0 * n
+        assert unit == "bytes" and amt == 34.0 * n
         assert ctx.time_steps(3) > 0
 
 
@@ -264,21 +274,23 @@ def test_beyond_2pow32_particles(gpu, orc):
     ext.shader_delay = 0
     chunk = 1 << 14
     starts = [0, (1 << 32) - chunk // 2, n - chunk]
-    fields = (rps.FIELD_X, rps.FIELD_Y, rps.FIELD_VX, rps.FIELD_VY, rps.FIELD_LIFE)
     with rps.Context(n) as ctx:
         ctx.set_config(cfg, ext)
         ctx.init_scatter(seed=3)
         ctx.step(1)
-        # force respawns inside the checked chunks
+        # force respawns inside the checked chunks (0.005 s = 1 step left)
         for s in starts:
             ctx.upload_field(rps.FIELD_LIFE, np.full(chunk, 0.005, F), s)
-        before = [{k: ctx.download_field(f, s, chunk) for k, f in zip(KEYS5, fields)} for s in starts]
+        before = [_download_chunk(rps, ctx, s, chunk) for s in starts]
         ctx.step(1)
-        after = [{k: ctx.download_field(f, s, chunk) for k, f in zip(KEYS5, fields)} for s in starts]
+        after = [_download_chunk(rps, ctx, s, chunk) for s in starts]
     for s, b, a in zip(starts, before, after):
+        assert (b["steps"] == 1).all()
+        b["exp"] = orc.exp_from_steps(b.pop("steps"), 1)
         st = orc.stream_step(cfg, ext, b, 1, id_offset=s, stats=True)
         assert st.respawned == chunk
-        assert_soa_bitwise(a, b, keys=KEYS5, what=f"chunk@{s} ")
+        b["steps"] = orc.steps_from_exp(b["exp"], 2)
+        assert_soa_bitwise(a, b, keys=KEYS_STEPS, what=f"chunk@{s} ")
 
 
 def test_render_export_matches_download(gpu):
@@ -308,3 +320,44 @@ def test_render_export_matches_download(gpu):
         with pytest.raises(rps.RpsError):
             host = np.zeros(n, rps.PARTICLE_DTYPE)
             ctx.export_particles(host.ctypes.data)  # host memory is rejected
+
+
+def test_lifetime_views_clock_and_toggle(gpu, orc):
+    """Lifetime kept as a u16 expiry on the lifetime clock: the seconds and
+    exact-steps views, and a lifetime clock that stands still while RPS_EXT_LIFETIME is off."""
+    rps = gpu
+    n = 10007
+    cfg = config_c1(rps, n)
+    ext = rps.headline_ext()
+    ext.shader_delay = 0
+    off = rps.headline_ext()
+    off.shader_delay = 0
+    off.flags = 0
+    dt = cfg.fixed_delta_time
+    soa = random_soa(n, list(cfg.screen_bounds), seed=51, life=(-0.05, 0.09))
+    with _gpu_ctx(rps, n, cfg, ext, soa) as ctx:
+        ref = copy_soa(soa)
+        ref["exp"] = orc.exp_from_life(ref["life"], 0, dt)
+        steps0 = ctx.download_field(rps.FIELD_LIFE_STEPS)
+        assert_bitwise(steps0, orc.steps_from_exp(ref["exp"], 0), "steps view")
+        assert_bitwise(ctx.download_field(rps.FIELD_LIFE), (steps0 * F(dt)).astype(F), "seconds view")
+        ctx.step(3)
+        for s in range(3):
+            orc.stream_step(cfg, ext, ref, s)
+        ctx.set_config(cfg, off)
+        frozen = ctx.download_field(rps.FIELD_LIFE_STEPS)
+        ctx.step(4)
+        for s in range(3, 7):
+            orc.stream_step(cfg, off, ref, s)
+        assert_bitwise(ctx.download_field(rps.FIELD_LIFE_STEPS), frozen, "clock stopped")
+        ctx.set_config(cfg, ext)
+        ctx.step(5)
+        for s in range(7, 12):
+            orc.stream_step(cfg, ext, ref, s, clock=s - 4)
+        got = ctx.download_soa()
+        assert_soa_bitwise(got, ref)
+        assert_bitwise(ctx.read_debug(rps.DEBUG_EXPIRY), ref["exp"], "expiry")
+        # exact round trip of the steps view (checkpoint / resume)
+        st = ctx.download_field(rps.FIELD_LIFE_STEPS)
+        ctx.upload_field(rps.FIELD_LIFE_STEPS, st)
+        assert_bitwise(ctx.read_debug(rps.DEBUG_EXPIRY), ref["exp"], "steps round trip")

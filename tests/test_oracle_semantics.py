@@ -49,7 +49,7 @@ def test_lifetime_respawn_matches_numpy(rps, orc):
     soa = random_soa(8192, list(cfg.screen_bounds), seed=14, life=(-0.5, 0.5))
     a, b = _run_both(orc, cfg, ext, soa, step=42, id_offset=123456789)
     assert (b["life"] > 0).all()
-    assert_soa_bitwise(a, b, keys=("x", "y", "vx", "vy", "life"))
+    assert_soa_bitwise(a, b, keys=("x", "y", "vx", "vy", "exp", "life"))
 
 
 def test_respawn_lands_in_emitter_disc(rps, orc):
@@ -60,7 +60,9 @@ def test_respawn_lands_in_emitter_disc(rps, orc):
     assert st.respawned == 4096
     r = np.hypot(soa["x"], soa["y"])
     assert (r <= 50.0 + 1e-3).all()
-    assert ((soa["life"] >= 1.0) & (soa["life"] <= 5.0)).all()
+    # lifetimes U(1, 5) s quantised to whole steps: ceil(L / dt) * dt
+    dt = cfg.fixed_delta_time
+    assert ((soa["life"] >= 1.0) & (soa["life"] <= 5.0 + dt)).all()
     spd = np.hypot(soa["vx"], soa["vy"])
     assert (spd <= 100.0 + 1e-3).all()
 
@@ -79,7 +81,7 @@ def test_sharded_equals_unsharded(rps, orc):
         s = {k: v[lo:hi].copy() for k, v in soa.items()}
         orc.stream_step(cfg, ext, s, 9, lo)
         parts.append(s)
-    for k in ("x", "y", "vx", "vy", "life"):
+    for k in ("x", "y", "vx", "vy", "exp", "life"):
         assert_bitwise(np.concatenate([p[k] for p in parts]), whole[k], k)
 
 
@@ -90,7 +92,7 @@ def test_omp_build_equals_serial(rps, orc):
     a, b = copy_soa(soa), copy_soa(soa)
     orc.stream_step(cfg, ext, a, 4)
     orc.stream_step_omp(cfg, ext, b, 4, threads=4)
-    assert_soa_bitwise(a, b, keys=("x", "y", "vx", "vy", "life"))
+    assert_soa_bitwise(a, b, keys=("x", "y", "vx", "vy", "exp"))
 
 
 def test_run_steps_gating(rps, orc):

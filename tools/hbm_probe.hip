@@ -148,6 +148,31 @@ __global__ __launch_bounds__(256) void flat_rmw_u_k(f4* a, size_t n4, float s) {
   for (int u = 0; u < U; ++u) if (base + u * 256 < n4) st<NT>(a + base + u * 256, r[u] * s + 1.0f);
 }
 
+// Expiry layout: tiles of T particles = 4 float segments + one u16 segment (T*18 B).
+// x,y,vx,vy read+written, the u16 expiry read (written only where it matches: never here).
+typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+template <int T, bool EXP>
+__global__ __launch_bounds__(256) void rmw4e_k(f4* base, size_t n4, float s, unsigned short key) {
+  size_t v = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= n4) return;
+  constexpr size_t T4 = T / 4;
+  const size_t tile = v / T4, w = v % T4;
+  f4* t = base + tile * (EXP ? 18 : 16) * T4 / 4 + w;  // tile stride in f4: T*18/16
+  f4 A = __builtin_nontemporal_load(t), B = __builtin_nontemporal_load(t + T4),
+     C = __builtin_nontemporal_load(t + 2 * T4), D = __builtin_nontemporal_load(t + 3 * T4);
+  bool hit = false;
+  if constexpr (EXP) {
+    const u16x4* e = reinterpret_cast<const u16x4*>(t - w + 4 * T4) + w;
+    u16x4 E = __builtin_nontemporal_load(e);
+    hit = E[0] == key || E[1] == key || E[2] == key || E[3] == key;
+  }
+  if (hit) A = A + 1.0f;
+  __builtin_nontemporal_store(A * s + B, t);
+  __builtin_nontemporal_store(B * s + C, t + T4);
+  __builtin_nontemporal_store(C * s + D, t + 2 * T4);
+  __builtin_nontemporal_store(D * s + A, t + 3 * T4);
+}
+
 // Same with 512-thread workgroups.
 template <bool NT, int T>
 __global__ __launch_bounds__(512) void rmw5_tiled_b512_k(f4* base, size_t n4, float s) {
@@ -257,6 +282,10 @@ int main(int argc, char** argv) {
     run("flat rmw u5", 40.0 * n, [&] { hipLaunchKernelGGL((flat_rmw_u_k<true, 5>), dim3((gf + 4) / 5), dim3(256), 0, 0, tb, f4n, 1.0f); });
     run("flat rmw u4", 40.0 * n, [&] { hipLaunchKernelGGL((flat_rmw_u_k<true, 4>), dim3((gf + 3) / 4), dim3(256), 0, 0, tb, f4n, 1.0f); });
     run("flat copy", 40.0 * n, [&] { hipLaunchKernelGGL(copy_k<true>, dim3(gf), dim3(256), 0, 0, tb, tb2, f4n); std::swap(tb, tb2); });
+    run("t8192 4f+u16", 34.0 * n, [&] { hipLaunchKernelGGL((rmw4e_k<8192, true>), dim3(g), dim3(256), 0, 0, tb, n4, 1.0f, (unsigned short)7); });
+    run("t8192 4f", 32.0 * n, [&] { hipLaunchKernelGGL((rmw4e_k<8192, false>), dim3(g), dim3(256), 0, 0, tb, n4, 1.0f, (unsigned short)7); });
+    run("t4096 4f+u16", 34.0 * n, [&] { hipLaunchKernelGGL((rmw4e_k<4096, true>), dim3(g), dim3(256), 0, 0, tb, n4, 1.0f, (unsigned short)7); });
+    run("t16384 4f+u16", 34.0 * n, [&] { hipLaunchKernelGGL((rmw4e_k<16384, true>), dim3(g), dim3(256), 0, 0, tb, n4, 1.0f, (unsigned short)7); });
     if (only_new) continue;
     run("rmw5 nt", 40.0 * n, [&] { hipLaunchKernelGGL(rmw5_k<true>, dim3(g), dim3(256), 0, 0, a, b, c, d, e, n4, 1.0f); });
     run("t1024 nt", 40.0 * n, [&] { hipLaunchKernelGGL((rmw5_tiled_k<true, 1024>), dim3(g), dim3(256), 0, 0, tb, n4, 1.0f); });

@@ -17,7 +17,7 @@ import rps_amd as rps  # noqa: E402
 
 N = int(os.environ.get("TUNE_N", 100_000_000))
 STEPS = 50
-ROUNDS = 4
+ROUNDS = int(os.environ.get("TUNE_ROUNDS", 4))
 
 
 def copy_ref(nbytes):
@@ -41,17 +41,23 @@ def copy_ref(nbytes):
 
 def main():
     variants = []
-    for nt in (3, 1, 2, 0):  # bit 0 nontemporal loads, bit 1 nontemporal stores
-        variants.append(dict(grid=0, nt=nt, lifetime=True))
-    variants.append(dict(grid=16384, nt=3, lifetime=True))
-    variants.append(dict(grid=0, nt=3, lifetime=False))
-    variants.append(dict(grid=0, nt=1, lifetime=False))
+    if os.environ.get("TUNE_SET") == "xcd":
+        for xcd in (1, 0):
+            variants.append(dict(grid=0, nt=3, lifetime=True, xcd=xcd))
+            variants.append(dict(grid=0, nt=3, lifetime=False, xcd=xcd))
+    else:
+        for nt in (3, 1, 2, 0):  # bit 0 nontemporal loads, bit 1 nontemporal stores
+            variants.append(dict(grid=0, nt=nt, lifetime=True))
+        variants.append(dict(grid=16384, nt=3, lifetime=True))
+        variants.append(dict(grid=0, nt=3, lifetime=False))
+        variants.append(dict(grid=0, nt=1, lifetime=False))
     results = {json.dumps(v, sort_keys=True): [] for v in variants}
     cfg = rps.default_particle_config(N, gravity=0.0)
     for r in range(ROUNDS):
         for v in variants:
             os.environ["RPS_STREAM_GRID"] = str(v["grid"])
             os.environ["RPS_STREAM_NT"] = str(v["nt"])
+            os.environ["RPS_STREAM_XCD"] = str(v.get("xcd", 1))
             ext = rps.headline_ext()
             ext.shader_delay = 0
             if not v["lifetime"]:
