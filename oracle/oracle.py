@@ -45,6 +45,7 @@ def lib(omp: bool = False) -> ctypes.CDLL:
         "orc_cell_key": (_U32, [ctypes.c_int32, ctypes.c_int32, _U32]),
         "orc_f32_to_i32": (ctypes.c_int32, [_F]),
         "orc_life_steps": (_U32, [_F, _F]),
+        "orc_inv_sqrt": (_F, [_F]),
         "orc_exp_from_life": (None, [_P, _U64, _U32, _F, _P]),
         "orc_life_from_exp": (None, [_P, _U64, _U32, _F, _P]),
         "orc_stream_step": (None, [_P, _P, _U64, _U64, _U32, _P, _P, _P, _P, _P, _U64, _P]),
@@ -113,6 +114,10 @@ def set_color_array(vx, vy, max_energy):
     out[:, 2] = np.where(lo, np.float32(1) - t_lo, np.float32(0))
     out[:, 3] = 1.0
     return out
+
+
+def inv_sqrt(r2):
+    return lib().orc_inv_sqrt(r2)
 
 
 def life_steps(life, dt):

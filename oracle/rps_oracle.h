@@ -50,6 +50,8 @@ int32_t orc_f32_to_i32(float v);
  * clock value of the step in which it respawns; L seconds last clamp(ceil(L/dt), 1, 65535)
  * steps.  Conversions at lifetime clock c (the clock of the next step). */
 uint32_t orc_life_steps(float life, float dt);
+/* The attractor force's 1/sqrt (bit trick + 3 Newton steps). */
+float orc_inv_sqrt(float r2);
 void orc_exp_from_life(const float* life, uint64_t n, uint32_t clock, float dt, uint16_t* exp);
 void orc_life_from_exp(const uint16_t* exp, uint64_t n, uint32_t clock, float dt, float* life);
 

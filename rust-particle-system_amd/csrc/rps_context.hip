@@ -196,9 +196,10 @@ StreamArgs make_stream_args(const rps_ctx* ctx, uint64_t k) {
   a.na = std::min<uint32_t>(e.num_attractors, RPS_MAX_ATTRACTORS);
   const double t = (double)k * (double)dt;
   for (uint32_t i = 0; i < a.na; ++i) {
-    attractor_pos(e.attractors[i], t, a.ax[i], a.ay[i]);
-    a.as[i] = e.attractors[i].strength;
-    a.ae2[i] = e.attractors[i].softening * e.attractors[i].softening;
+    float px, py;
+    attractor_pos(e.attractors[i], t, px, py);
+    a.att[i] = f4{px, py, e.attractors[i].strength,
+                  e.attractors[i].softening * e.attractors[i].softening};
   }
   a.x_min = c.screen_bounds[0];
   a.x_max = c.screen_bounds[1];
@@ -311,8 +312,11 @@ int step_stream_fused(rps_ctx* ctx, uint64_t k0, uint32_t m, bool stats, uint64_
   fa.nsub = m;
   const double dt = (double)ctx->cfg.fixed_delta_time;
   for (uint32_t sub = 0; sub < m; ++sub)
-    for (uint32_t i = 0; i < fa.base.na; ++i)
-      attractor_pos(e.attractors[i], (double)(k0 + sub) * dt, fa.ax[sub][i], fa.ay[sub][i]);
+    for (uint32_t i = 0; i < fa.base.na; ++i) {
+      float px, py;
+      attractor_pos(e.attractors[i], (double)(k0 + sub) * dt, px, py);
+      fa.att[sub][i] = f4{px, py, fa.base.att[i][2], fa.base.att[i][3]};
+    }
   StreamLaunch l;
   l.verlet = e.integrator == RPS_INTEGRATOR_VERLET;
   l.lifetime = (e.flags & RPS_EXT_LIFETIME) != 0;

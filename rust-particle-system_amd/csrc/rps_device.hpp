@@ -84,7 +84,10 @@ struct StreamArgs {
   float dt, gx_dt, gy_dt, neg_g, half_dt, half_dt2, drag_f;
   uint32_t drag_on;
   uint32_t na;
-  float ax[kMaxAttractors], ay[kMaxAttractors], as[kMaxAttractors], ae2[kMaxAttractors];
+  // Attractors of this step {x, y, strength, softening^2}.  Kernels read them through the
+  // kernarg segment pointer with a uniform loop index (s_load_dwordx4 per attractor), so
+  // they neither occupy ~32 SGPRs for the whole kernel nor get indexed through scratch.
+  f4 att[kMaxAttractors];
   float x_min, x_max, y_min, y_max, damping;
   float emit_cx, emit_cy, emit_r, spd_min, spd_range, life_min, life_range;
   uint32_t key0, key1, step_lo, step_hi;
@@ -98,8 +101,7 @@ constexpr int kMaxFuse = 16;
 struct FusedArgs {
   StreamArgs base;  // step_lo/step_hi = first substep's active-step index
   uint32_t nsub;
-  float ax[kMaxFuse][kMaxAttractors];
-  float ay[kMaxFuse][kMaxAttractors];
+  f4 att[kMaxFuse][kMaxAttractors];  // per-substep attractors (base.att unused)
 };
 
 struct StatsPartial {  // 48 B, written once per workgroup, reduced in fixed order
@@ -234,22 +236,42 @@ __device__ __forceinline__ int32_t f32_to_i32(float v) {
   return (int32_t)v;
 }
 
-// Sum of attractor accelerations at (x, y), attractors in index order.
-// (apx, apy) are this step's attractor positions.
-__device__ __forceinline__ void attract(const StreamArgs& a, const float* apx, const float* apy,
-                                        float x, float y, float& ax, float& ay) {
-  float sx = 0.0f, sy = 0.0f;
+// 1/sqrt(r2) as specified in DESIGN.md §3.2: the bit-level initial guess 0x5f375a86 -
+// (bits(r2) >> 1) and three Newton steps y = y * (1.5 - (h * y) * y), h = 0.5 * r2, every
+// step a separately rounded IEEE f32 op (about 2 ulp from the true value).  Cheap on the
+// VALU (v_pk_mul/add on particle pairs, no v_sqrt/v_div sequences) and exactly the same
+// bits as the CPU oracle's orc_inv_sqrt.  Two particles at a time (f2 lanes).
+typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+// Uniform attractor table in the kernarg (constant) address space: loads are s_load.
+typedef __attribute__((address_space(4))) const f4* att_ptr;
+__device__ __forceinline__ f2 inv_sqrt_nr(f2 r2) {
+  const u2 b = __builtin_bit_cast(u2, r2);
+  f2 y = __builtin_bit_cast(f2, u2{0x5f375a86u, 0x5f375a86u} - (b >> 1u));
+  const f2 h = 0.5f * r2;
 #pragma unroll
-  for (int k = 0; k < kMaxAttractors; ++k) {
-    if ((uint32_t)k < a.na) {
-      const float dx = apx[k] - x;
-      const float dy = apy[k] - y;
-      const float r2 = (dx * dx + dy * dy) + a.ae2[k];
-      const float inv = 1.0f / sqrtf(r2);
-      const float s = a.as[k] * ((inv * inv) * inv);
-      sx = sx + dx * s;
-      sy = sy + dy * s;
-    }
+  for (int it = 0; it < 3; ++it) {
+    f2 t = h * y;
+    t = t * y;
+    t = 1.5f - t;
+    y = y * t;
+  }
+  return y;
+}
+
+// Sum of attractor accelerations at two particles (x, y), attractors in index order
+// (DESIGN.md §3.2).  att: this step's {x, y, strength, softening^2} (uniform, kernarg).
+__device__ __forceinline__ void attract2(att_ptr att, uint32_t na, f2 x, f2 y,
+                                         f2& ax, f2& ay) {
+  f2 sx = {0.0f, 0.0f}, sy = {0.0f, 0.0f};
+  for (uint32_t k = 0; k < na; ++k) {
+    const f4 A = att[k];
+    const f2 dx = A[0] - x;
+    const f2 dy = A[1] - y;
+    const f2 r2 = (dx * dx + dy * dy) + A[3];
+    const f2 inv = inv_sqrt_nr(r2);
+    const f2 s = A[2] * ((inv * inv) * inv);
+    sx = sx + dx * s;
+    sy = sy + dy * s;
   }
   ax = sx;
   ay = sy;
@@ -272,21 +294,25 @@ __device__ __forceinline__ uint32_t respawn(const StreamArgs& a, uint64_t step, 
   return life_steps(a.life_min + u01(w[2]) * a.life_range, a.dt);
 }
 
-// One particle, one active step.  Returns true when the particle respawned.
-// (apx, apy): attractor positions of this step; step: its active-step index (Philox counter);
-// clock: its lifetime-clock value; e: the particle's expiry (the clock value of the step in
-// which it respawns, mod 2^16).
+// Two particles, one active step (the kernels' unit: every op on the pair is one v_pk_*
+// where the ISA has it).  gid: global id of element 0 (element 1 is gid + 1).  Writes
+// re[i] = element i respawned.  With `single`, element 1 duplicates element 0 and only
+// element 0's lifetime is advanced (n % 4 tails).
+// att: this step's attractors; step: its active-step index (Philox counter); clock: its
+// lifetime-clock value; e[i]: expiries (the clock value of the step in which each
+// particle respawns, mod 2^16).
 template <bool VERLET, bool LIFETIME>
-__device__ __forceinline__ bool step_one(const StreamArgs& a, const float* apx, const float* apy,
-                                         uint64_t step, uint32_t clock, uint64_t gid, float& x,
-                                         float& y, float& vx, float& vy, uint16_t& e) {
+__device__ __forceinline__ void step_pair(const StreamArgs& a, att_ptr att,
+                                          uint64_t step, uint32_t clock, uint64_t gid, f2& x,
+                                          f2& y, f2& vx, f2& vy, uint16_t e[2], bool re[2],
+                                          bool single = false) {
   const float dt = a.dt;
   if constexpr (!VERLET) {
     vx = vx + a.gx_dt;  // apply_gravity, wgsl:397-400
     vy = vy + a.gy_dt;
     if (a.na) {
-      float ax, ay;
-      attract(a, apx, apy, x, y, ax, ay);
+      f2 ax, ay;
+      attract2(att, a.na, x, y, ax, ay);
       vx = vx + ax * dt;
       vy = vy + ay * dt;
     }
@@ -297,12 +323,12 @@ __device__ __forceinline__ bool step_one(const StreamArgs& a, const float* apx, 
     x = x + vx * dt;  // update_particle_positions, wgsl:392-395
     y = y + vy * dt;
   } else {
-    float ax0, ay0, ax1, ay1;
-    attract(a, apx, apy, x, y, ax0, ay0);
+    f2 ax0, ay0, ax1, ay1;
+    attract2(att, a.na, x, y, ax0, ay0);
     ay0 = ay0 + a.neg_g;
-    const float x1 = (x + vx * dt) + ax0 * a.half_dt2;
-    const float y1 = (y + vy * dt) + ay0 * a.half_dt2;
-    attract(a, apx, apy, x1, y1, ax1, ay1);
+    const f2 x1 = (x + vx * dt) + ax0 * a.half_dt2;
+    const f2 y1 = (y + vy * dt) + ay0 * a.half_dt2;
+    attract2(att, a.na, x1, y1, ax1, ay1);
     ay1 = ay1 + a.neg_g;
     vx = vx + (ax0 + ax1) * a.half_dt;
     vy = vy + (ay0 + ay1) * a.half_dt;
@@ -313,14 +339,22 @@ __device__ __forceinline__ bool step_one(const StreamArgs& a, const float* apx, 
     x = x1;
     y = y1;
   }
-  wall(a.x_min, a.x_max, a.y_min, a.y_max, a.damping, x, y, vx, vy);
-  if constexpr (LIFETIME) {
-    if (e == (uint16_t)clock) {
-      e = (uint16_t)(clock + respawn(a, step, gid, x, y, vx, vy));
-      return true;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    float px = x[i], py = y[i], qx = vx[i], qy = vy[i];
+    wall(a.x_min, a.x_max, a.y_min, a.y_max, a.damping, px, py, qx, qy);
+    re[i] = false;
+    if constexpr (LIFETIME) {
+      if ((i == 0 || !single) && e[i] == (uint16_t)clock) {
+        e[i] = (uint16_t)(clock + respawn(a, step, gid + i, px, py, qx, qy));
+        re[i] = true;
+      }
     }
+    x[i] = px;
+    y[i] = py;
+    vx[i] = qx;
+    vy[i] = qy;
   }
-  return false;
 }
 
 }  // namespace rps

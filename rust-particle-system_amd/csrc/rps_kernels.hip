@@ -131,13 +131,76 @@ __device__ __forceinline__ uint64_t stream_block(const StreamArgs& a, uint32_t b
   return (uint64_t)x * q + (x < r ? x : r) + k;
 }
 
+// The attractor table inside this launch's kernarg segment (see StreamArgs::att).
+template <class Args>
+__device__ __forceinline__ att_ptr kernarg_f4(size_t offset) {
+  typedef __attribute__((address_space(4))) const char* kchar;
+  return (att_ptr)((kchar)__builtin_amdgcn_kernarg_segment_ptr() + offset);
+}
+
+// Four particles of one lane (two f2 pairs) through `nsub` steps in registers.
+template <bool VERLET, bool LIFETIME>
+__device__ __forceinline__ void step_quad(const StreamArgs& a, att_ptr att0, size_t att_stride,
+                                          uint32_t nsub, uint64_t step0, uint32_t clock0,
+                                          uint64_t gid, f4& X, f4& Y, f4& VX, f4& VY, h4& E,
+                                          bool re[4], bool& any) {
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    f2 x = {X[2 * p], X[2 * p + 1]}, y = {Y[2 * p], Y[2 * p + 1]};
+    f2 vx = {VX[2 * p], VX[2 * p + 1]}, vy = {VY[2 * p], VY[2 * p + 1]};
+    uint16_t e[2] = {E[2 * p], E[2 * p + 1]};
+    bool r[2] = {false, false};
+    for (uint32_t sub = 0; sub < nsub; ++sub) {
+      step_pair<VERLET, LIFETIME>(a, att0 + sub * att_stride, step0 + sub, clock0 + sub,
+                                  gid + 2 * p, x, y, vx, vy, e, r);
+      any |= r[0] | r[1];
+    }
+    X[2 * p] = x[0];
+    X[2 * p + 1] = x[1];
+    Y[2 * p] = y[0];
+    Y[2 * p + 1] = y[1];
+    VX[2 * p] = vx[0];
+    VX[2 * p + 1] = vx[1];
+    VY[2 * p] = vy[0];
+    VY[2 * p + 1] = vy[1];
+    E[2 * p] = e[0];
+    E[2 * p + 1] = e[1];
+    re[2 * p] = r[0];
+    re[2 * p + 1] = r[1];
+  }
+}
+
+// One particle (n % 4 tails) through `nsub` steps: the pair path with element 1 a copy.
+template <bool VERLET, bool LIFETIME>
+__device__ __forceinline__ bool step_single(const StreamArgs& a, att_ptr att0, size_t att_stride,
+                                            uint32_t nsub, uint64_t step0, uint32_t clock0,
+                                            uint64_t gid, float& px, float& py, float& qx,
+                                            float& qy, uint16_t& pe, bool& any) {
+  f2 x = {px, px}, y = {py, py}, vx = {qx, qx}, vy = {qy, qy};
+  uint16_t e[2] = {pe, pe};
+  bool r[2] = {false, false};
+  for (uint32_t sub = 0; sub < nsub; ++sub) {
+    step_pair<VERLET, LIFETIME>(a, att0 + sub * att_stride, step0 + sub, clock0 + sub, gid, x, y,
+                                vx, vy, e, r, true);
+    any |= r[0];
+  }
+  px = x[0];
+  py = y[0];
+  qx = vx[0];
+  qy = vy[0];
+  pe = e[0];
+  return r[0];
+}
+
+// Shared body of the one-step and the temporally fused kernels.
 template <bool VERLET, bool LIFETIME, bool STATS, int NTM>
-__global__ __launch_bounds__(kBlock) void stream_step_kernel(StreamArgs a) {
+__device__ __forceinline__ void stream_body(const StreamArgs& a, att_ptr att0, size_t att_stride,
+                                            uint32_t nsub) {
   constexpr bool NTL = (NTM & 1) != 0, NTS = (NTM & 2) != 0;
   const uint64_t nvec = a.n >> 2;
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
   const uint64_t tid = stream_block(a, blockIdx.x) * kBlock + threadIdx.x;
-  const uint64_t step = ((uint64_t)a.step_hi << 32) | a.step_lo;
+  const uint64_t step0 = ((uint64_t)a.step_hi << 32) | a.step_lo;
   StatsAcc acc;
   if constexpr (STATS) acc.init();
   for (uint64_t v = tid; v < nvec; v += stride) {
@@ -149,20 +212,12 @@ __global__ __launch_bounds__(kBlock) void stream_step_kernel(StreamArgs a) {
     f4 VY = ld4<NTL>(a.vy + o);
     h4 E = {0, 0, 0, 0};
     if constexpr (LIFETIME) E = lde4<NTL>(a.exp + eidx(i));
-    bool any = false;
+    bool re[4], any = false;
+    step_quad<VERLET, LIFETIME>(a, att0, att_stride, nsub, step0, a.clock, a.id_offset + i, X, Y, VX,
+                                VY, E, re, any);
+    if constexpr (STATS) {
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      float x = X[c], y = Y[c], vx = VX[c], vy = VY[c];
-      uint16_t e = E[c];
-      const bool re = step_one<VERLET, LIFETIME>(a, a.ax, a.ay, step, a.clock, a.id_offset + i + c, x,
-                                                 y, vx, vy, e);
-      X[c] = x;
-      Y[c] = y;
-      VX[c] = vx;
-      VY[c] = vy;
-      E[c] = e;
-      any |= re;
-      if constexpr (STATS) acc.add(x, y, vx, vy, re);
+      for (int c = 0; c < 4; ++c) acc.add(X[c], Y[c], VX[c], VY[c], re[c]);
     }
     st4<NTS>(a.x + o, X);
     st4<NTS>(a.y + o, Y);
@@ -179,83 +234,9 @@ __global__ __launch_bounds__(kBlock) void stream_step_kernel(StreamArgs a) {
     const uint64_t o = tidx(i);
     float x = a.x[o], y = a.y[o], vx = a.vx[o], vy = a.vy[o];
     uint16_t e = LIFETIME ? a.exp[eidx(i)] : 0;
-    const bool re = step_one<VERLET, LIFETIME>(a, a.ax, a.ay, step, a.clock, a.id_offset + i, x, y, vx,
-                                               vy, e);
-    a.x[o] = x;
-    a.y[o] = y;
-    a.vx[o] = vx;
-    a.vy[o] = vy;
-    if constexpr (LIFETIME) {
-      if (re) a.exp[eidx(i)] = e;
-    }
-    if constexpr (STATS) acc.add(x, y, vx, vy, re);
-  }
-  if constexpr (STATS) block_reduce_stats(acc, a.partials);
-}
-
-// Temporal fusion: the same per-particle step applied nsub times in registers, state read
-// and written once (DESIGN.md §5).  Particles are independent, so this is bitwise equal to
-// nsub separate launches; stats (if any) reduce the final substep's state.
-template <bool VERLET, bool LIFETIME, bool STATS, int NTM>
-__global__ __launch_bounds__(kBlock) void stream_fused_kernel(FusedArgs fa) {
-  constexpr bool NTL = (NTM & 1) != 0, NTS = (NTM & 2) != 0;
-  const StreamArgs& a = fa.base;
-  const uint64_t nvec = a.n >> 2;
-  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-  const uint64_t tid = stream_block(a, blockIdx.x) * kBlock + threadIdx.x;
-  const uint64_t step0 = ((uint64_t)a.step_hi << 32) | a.step_lo;
-  StatsAcc acc;
-  if constexpr (STATS) acc.init();
-  for (uint64_t v = tid; v < nvec; v += stride) {
-    const uint64_t i = v << 2;
-    const uint64_t o = tidx(i);
-    f4 X = ld4<NTL>(a.x + o);
-    f4 Y = ld4<NTL>(a.y + o);
-    f4 VX = ld4<NTL>(a.vx + o);
-    f4 VY = ld4<NTL>(a.vy + o);
-    h4 E = {0, 0, 0, 0};
-    if constexpr (LIFETIME) E = lde4<NTL>(a.exp + eidx(i));
-    bool re[4] = {false, false, false, false};
     bool any = false;
-    for (uint32_t sub = 0; sub < fa.nsub; ++sub) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        float x = X[c], y = Y[c], vx = VX[c], vy = VY[c];
-        uint16_t e = E[c];
-        re[c] = step_one<VERLET, LIFETIME>(a, fa.ax[sub], fa.ay[sub], step0 + sub, a.clock + sub,
-                                           a.id_offset + i + c, x, y, vx, vy, e);
-        X[c] = x;
-        Y[c] = y;
-        VX[c] = vx;
-        VY[c] = vy;
-        E[c] = e;
-        any |= re[c];
-      }
-    }
-    if constexpr (STATS) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) acc.add(X[c], Y[c], VX[c], VY[c], re[c]);
-    }
-    st4<NTS>(a.x + o, X);
-    st4<NTS>(a.y + o, Y);
-    st4<NTS>(a.vx + o, VX);
-    st4<NTS>(a.vy + o, VY);
-    if constexpr (LIFETIME) {
-      if (any) ste4<NTS>(a.exp + eidx(i), E);
-    }
-  }
-  const uint64_t rem = a.n - (nvec << 2);
-  if (tid < rem) {
-    const uint64_t i = (nvec << 2) + tid;
-    const uint64_t o = tidx(i);
-    float x = a.x[o], y = a.y[o], vx = a.vx[o], vy = a.vy[o];
-    uint16_t e = LIFETIME ? a.exp[eidx(i)] : 0;
-    bool re = false, any = false;
-    for (uint32_t sub = 0; sub < fa.nsub; ++sub) {
-      re = step_one<VERLET, LIFETIME>(a, fa.ax[sub], fa.ay[sub], step0 + sub, a.clock + sub,
-                                      a.id_offset + i, x, y, vx, vy, e);
-      any |= re;
-    }
+    const bool re = step_single<VERLET, LIFETIME>(a, att0, att_stride, nsub, step0, a.clock,
+                                                  a.id_offset + i, x, y, vx, vy, e, any);
     a.x[o] = x;
     a.y[o] = y;
     a.vx[o] = vx;
@@ -266,6 +247,20 @@ __global__ __launch_bounds__(kBlock) void stream_fused_kernel(FusedArgs fa) {
     if constexpr (STATS) acc.add(x, y, vx, vy, re);
   }
   if constexpr (STATS) block_reduce_stats(acc, a.partials);
+}
+
+template <bool VERLET, bool LIFETIME, bool STATS, int NTM>
+__global__ __launch_bounds__(kBlock) void stream_step_kernel(StreamArgs a) {
+  stream_body<VERLET, LIFETIME, STATS, NTM>(a, kernarg_f4<StreamArgs>(offsetof(StreamArgs, att)), 0, 1);
+}
+
+// Temporal fusion: the same per-particle step applied nsub times in registers, state read
+// and written once (DESIGN.md §5).  Particles are independent, so this is bitwise equal to
+// nsub separate launches; stats (if any) reduce the final substep's state.
+template <bool VERLET, bool LIFETIME, bool STATS, int NTM>
+__global__ __launch_bounds__(kBlock) void stream_fused_kernel(FusedArgs fa) {
+  stream_body<VERLET, LIFETIME, STATS, NTM>(fa.base, kernarg_f4<FusedArgs>(offsetof(FusedArgs, att)),
+                                            kMaxAttractors, fa.nsub);
 }
 
 // First level of the fixed-order partial reduction: workgroup b folds partials

@@ -75,6 +75,19 @@ def attractor_positions(ext, active_step):
     return out
 
 
+def inv_sqrt(r2):
+    """bit-level guess 0x5f375a86 - (bits >> 1), three f32 Newton steps."""
+    r2 = np.asarray(r2, F)
+    y = (np.uint32(0x5f375a86) - (r2.view(np.uint32) >> np.uint32(1))).astype(np.uint32).view(F)
+    h = F(0.5) * r2
+    for _ in range(3):
+        t = h * y
+        t = t * y
+        t = F(1.5) - t
+        y = y * t
+    return y
+
+
 def attract(atts, x, y):
     sx = np.zeros_like(x)
     sy = np.zeros_like(y)
@@ -82,7 +95,7 @@ def attract(atts, x, y):
         dx = px - x
         dy = py - y
         r2 = (dx * dx + dy * dy) + e2
-        inv = F(1.0) / np.sqrt(r2)
+        inv = inv_sqrt(r2)
         s = st * ((inv * inv) * inv)
         sx = sx + dx * s
         sy = sy + dy * s

@@ -103,3 +103,30 @@ def test_set_color_known_answers(orc):
     for i in range(0, 2000, 97):
         assert np.array_equal(orc.set_color(float(vx[i]), float(vy[i]), 2000.0).view(np.uint32),
                               vec[i].view(np.uint32))
+
+
+def test_attractor_inv_sqrt_accuracy(orc):
+    """The attractor force's 1/sqrt (bit guess + 3 Newton steps) is within
+    2.5 ulp of the exact value over 60 decades, and the C oracle equals the numpy restatement."""
+    import ref_numpy as RN
+
+    g = np.random.default_rng(3)
+    r = np.exp(g.uniform(np.log(1e-30), np.log(1e30), 200_000)).astype(np.float32)
+    y = RN.inv_sqrt(r)
+    exact = 1.0 / np.sqrt(r.astype(np.float64))
+    ulp = np.spacing(exact.astype(np.float32)).astype(np.float64)
+    assert (np.abs(y.astype(np.float64) - exact) / ulp).max() <= 2.5
+    for v in r[:2000]:
+        assert np.float32(orc.inv_sqrt(float(v))).view(np.uint32) == RN.inv_sqrt(np.array([v], np.float32)).view(np.uint32)[0]
+
+
+def test_life_steps_kat(orc):
+    """Lifetime quantisation clamp(ceil(L/dt), 1, 65535)."""
+    dt = np.float32(0.01)
+    assert orc.life_steps(0.0, dt) == 1
+    assert orc.life_steps(-3.0, dt) == 1
+    assert orc.life_steps(float("nan"), dt) == 1
+    assert orc.life_steps(1e9, dt) == 65535
+    assert orc.life_steps(0.005, dt) == 1
+    assert orc.life_steps(1.0, dt) == int(np.ceil(np.float32(1.0) / dt))
+    assert orc.life_steps(5.0, dt) == int(np.ceil(np.float32(5.0) / dt))
