@@ -24,7 +24,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "gpurun_out")
 PROF = os.path.join(ROOT, "profiles")
 WORKLOAD = "C3-1e8-4att-drag-respawn-euler"
-DOMINANT = "stream_step_kernel<false, true, false, true>"
+DOMINANT = "stream_step_kernel<false, true, false, 3>"
 
 
 def main(tag):
