@@ -387,7 +387,6 @@ int step_nbody(rps_ctx* ctx) {
 
 int step_sph_grid(rps_ctx* ctx) {
   SphBuffers b = sph_buffers(ctx);
-  RPS_HIP(ctx, launch_sph_bin(b, ctx->stream));
   RPS_HIP(ctx, launch_sph_sort(b, ctx->stream, &ctx->sort_passes, &ctx->sort_launches));
   RPS_HIP(ctx, launch_sph_offsets(b, ctx->stream));
   return RPS_OK;
@@ -510,9 +509,9 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     slots.push_back({(void**)&ctx->vy2, nf});
     slots.push_back({(void**)&ctx->x2, nf});
     slots.push_back({(void**)&ctx->y2, nf});
-    slots.push_back({(void**)&ctx->pred_s, align_up(n * sizeof(f2), 256)});
-    slots.push_back({(void**)&ctx->vel_s, align_up(n * sizeof(f2), 256)});
-    slots.push_back({(void**)&ctx->dens_s, align_up(n * sizeof(f2), 256)});
+    slots.push_back({(void**)&ctx->pred_s, align_up((size_t)ctx->P * sizeof(f2), 256)});
+    slots.push_back({(void**)&ctx->vel_s, align_up((size_t)ctx->P * sizeof(f2), 256)});
+    slots.push_back({(void**)&ctx->dens_s, align_up((size_t)ctx->P * sizeof(f2), 256)});
     slots.push_back({(void**)&ctx->lookup, align_up((size_t)ctx->P * sizeof(uint2), 256)});
     slots.push_back({(void**)&ctx->offsets, align_up(n * sizeof(uint32_t), 256)});
     slots.push_back({(void**)&ctx->dens, align_up(n * sizeof(f2), 256)});

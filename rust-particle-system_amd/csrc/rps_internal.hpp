@@ -99,13 +99,12 @@ struct SphBuffers {
   // Neighbour data gathered into spatial-lookup order (entry j holds particle lookup[j].y's
   // value), so a cell's entries are contiguous: pred_s/vel_s after prediction, dens_s after
   // the density pass.
-  f2* pred_s;        // N
-  f2* vel_s;         // N
-  f2* dens_s;        // N
+  f2* pred_s;        // P (every lookup slot)
+  f2* vel_s;         // P
+  f2* dens_s;        // P
   uint32_t n;        // N
   uint32_t p;        // next_pow2(N)
 };
-hipError_t launch_sph_bin(const SphBuffers& b, hipStream_t s);
 // Runs the whole bitonic network of src/particle_compute.rs:117-149; returns the number of
 // reference passes covered (S(S+1)/2) in *passes.
 hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,

@@ -5,6 +5,9 @@
 // kernel: DESIGN.md §4-§5.  Built with -ffp-contract=off (see rps_device.hpp).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "rps_internal.hpp"
 
 namespace rps {
@@ -546,78 +549,151 @@ __global__ __launch_bounds__(kBlock) void nbody_integrate_kernel(NbodyIntegrateA
 // SPH: the reference's five passes
 // ---------------------------------------------------------------------------------------
 
-// bin_particles_in_grid, compute_shader.wgsl:455-468 (+ :121-142).
-__global__ __launch_bounds__(kBlock) void sph_bin_kernel(const rps_config* __restrict__ cfg,
-                                                         const float* __restrict__ x,
-                                                         const float* __restrict__ y,
-                                                         uint2* __restrict__ lookup,
-                                                         uint32_t* __restrict__ offsets,
-                                                         uint32_t n) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  const float r = cfg->smoothing_radius;
-  const int32_t cx = f32_to_i32((x[i] + cfg->screen_bounds[1]) / r);
-  const int32_t cy = f32_to_i32((y[i] + cfg->screen_bounds[3]) / r);
-  lookup[i] = make_uint2(cell_key(cx, cy, cfg->particle_count), i);
-  offsets[i] = 0xFFFFFFFFu;
-}
-
-// sort_particles, compute_shader.wgsl:470-505: one compare-swap of pair i of the pass
-// (group_width gw; flip = step_index == 0).
-__device__ __forceinline__ void bitonic_pair(uint32_t i, uint32_t gw, bool flip, uint32_t& left,
-                                             uint32_t& right) {
-  const uint32_t gh = 2u * gw - 1u;
-  const uint32_t h = i & (gw - 1u);
-  left = h + (gh + 1u) * (i / gw);
-  right = left + (flip ? gh - 2u * h : (gh + 1u) / 2u);
-}
-
-// One global pass (group_width >= LDS tile): P/2 threads.
-__global__ __launch_bounds__(kBlock) void sph_sort_global_kernel(uint2* __restrict__ lookup,
-                                                                 uint32_t p, uint32_t gw,
-                                                                 uint32_t flip) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= p / 2u) return;
-  uint32_t l, r;
-  bitonic_pair(i, gw, flip != 0, l, r);
-  if (r >= p) return;
-  const uint2 a = lookup[l], b = lookup[r];
-  if (a.x > b.x) {
-    lookup[l] = b;
-    lookup[r] = a;
+// sort_particles, compute_shader.wgsl:470-505: pass (group_width gw, flip = step_index == 0)
+// pairs left = h + 2gw*(i/gw), h = i % gw, with right = left + (flip ? 2gw-1-2h : gw) and
+// swaps the (key, index) entries when key(left) > key(right).
+// Several consecutive passes of one stage in registers.  Passes t..t+K-1 of a stage have
+// strides G, G/2, ..., g = G / 2^(K-1) (stride = group_width).  For a residue r < g the
+// 2^K entries r + j*g (j < 2^K) of a 2G block are closed under the non-flip passes (stride
+// g*2^m pairs j with j + 2^m), and with a flip first pass (pairs h <-> 2G-1-h) the class r
+// together with its mirror class g-1-r (2^(K+1) entries, r < g/2) is closed as well.  One
+// thread loads its group, applies the K passes in network order (flip first, then
+// descending strides) with the reference's compare-swap, and stores it back: the same
+// network, the same comparisons, so the same result as K pass-per-dispatch launches.
+// `mem` is the lookup (global passes) or the workgroup's LDS tile (local passes).
+template <int K, bool FLIP, class T>
+__device__ __forceinline__ void sort_group(T* mem, uint32_t base, uint32_t r, uint32_t g) {
+  constexpr int M = 1 << K;            // entries per residue class
+  constexpr int E = FLIP ? 2 * M : M;  // entries per group
+  uint2 v[E];
+#pragma unroll
+  for (int j = 0; j < M; ++j) v[j] = mem[base + r + j * g];
+  if constexpr (FLIP) {
+#pragma unroll
+    for (int j = 0; j < M; ++j) v[M + j] = mem[base + (g - 1u - r) + j * g];
+    // flip pass: position r + j*g pairs with 2G-1-(r + j*g) = (g-1-r) + (M-1-j)*g.
+#pragma unroll
+    for (int j = 0; j < M / 2; ++j) {
+      uint2& lo = v[j];  // position < G: the left entry
+      uint2& hi = v[M + (M - 1 - j)];
+      if (lo.x > hi.x) { const uint2 tmp = lo; lo = hi; hi = tmp; }
+      uint2& lo2 = v[M + j];  // mirror class, position (g-1-r) + j*g < G
+      uint2& hi2 = v[M - 1 - j];
+      if (lo2.x > hi2.x) { const uint2 tmp = lo2; lo2 = hi2; hi2 = tmp; }
+    }
   }
+  // Non-flip passes, strides g*2^m for m = (FLIP ? K-2 : K-1) down to 0, in each class.
+#pragma unroll
+  for (int m = (FLIP ? K - 2 : K - 1); m >= 0; --m) {
+#pragma unroll
+    for (int c = 0; c < E / M; ++c) {
+#pragma unroll
+      for (int j = 0; j < M; ++j) {
+        if (j & (1 << m)) continue;
+        uint2& a = v[c * M + j];
+        uint2& b = v[c * M + j + (1 << m)];
+        if (a.x > b.x) { const uint2 tmp = a; a = b; b = tmp; }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < M; ++j) mem[base + r + j * g] = v[j];
+  if constexpr (FLIP) {
+#pragma unroll
+    for (int j = 0; j < M; ++j) mem[base + (g - 1u - r) + j * g] = v[M + j];
+  }
+}
+
+// Groups of a (K, flip) chunk in an array of `len` entries, group q -> (base, residue).
+__device__ __forceinline__ uint32_t sort_groups(uint32_t len, uint32_t G, uint32_t g, bool flip) {
+  return (len / (2u * G)) * (flip ? g / 2u : g);
+}
+__device__ __forceinline__ void sort_group_at(uint32_t q, uint32_t G, uint32_t g, bool flip,
+                                              uint32_t& base, uint32_t& r) {
+  const uint32_t per = flip ? g / 2u : g;
+  base = (q / per) * 2u * G;
+  r = q % per;
+}
+
+// K global passes of one stage, one group per thread.
+template <int K, bool FLIP>
+__global__ __launch_bounds__(kBlock) void sph_sort_fused_kernel(uint2* __restrict__ lookup,
+                                                                uint32_t p, uint32_t G) {
+  const uint32_t g = G >> (K - 1);
+  const uint32_t q = blockIdx.x * kBlock + threadIdx.x;
+  if (q >= sort_groups(p, G, g, FLIP)) return;
+  uint32_t base, r;
+  sort_group_at(q, G, g, FLIP, base, r);
+  sort_group<K, FLIP>(lookup, base, r, g);
 }
 
 constexpr uint32_t kSortTile = 8192;  // entries per workgroup tile (64 KiB of LDS)
+constexpr uint32_t kSortFuse = 4;     // global passes per register-fused launch
+
+// bin_particles_in_grid (wgsl:455-468) folded into the first sort launch: entries [0, n)
+// get (key, i) from the current positions and offsets[i] <- 0xFFFFFFFF; entries [n, P) keep
+// what the previous frame's sort left there (the reference never rewrites them).
+struct SortBin {
+  const rps_config* cfg;
+  const float* x;
+  const float* y;
+  uint32_t* offsets;
+  uint32_t n;
+};
+
+__device__ __forceinline__ uint2 bin_entry(const SortBin& b, uint32_t i) {
+  const float r = b.cfg->smoothing_radius;
+  const int32_t cx = f32_to_i32((b.x[i] + b.cfg->screen_bounds[1]) / r);
+  const int32_t cy = f32_to_i32((b.y[i] + b.cfg->screen_bounds[3]) / r);
+  b.offsets[i] = 0xFFFFFFFFu;
+  return make_uint2(cell_key(cx, cy, b.cfg->particle_count), i);
+}
 
 // Every remaining pass of stages [stage_lo, stage_hi] whose group_width fits one tile:
 // a pass with 2*gw <= tile only pairs entries inside aligned blocks of 2*gw, so a tile of
-// the array can run it on its own.  Same network, same compare order per pair -> identical
+// the array can run it on its own.  Passes go in register chunks (sort_group) of up to 3
+// (flip first: up to 2) per barrier; same network, same compare order per pair -> identical
 // result to the reference's pass-per-dispatch schedule.
-__global__ __launch_bounds__(1024) void sph_sort_local_kernel(uint2* __restrict__ lookup,
-                                                              uint32_t tile, uint32_t stage_lo,
-                                                              uint32_t stage_hi,
-                                                              uint32_t first_step) {
+template <bool BIN, int KMAX>
+__global__ __launch_bounds__(1024) void sph_sort_local_kernel(
+    uint2* __restrict__ lookup, uint32_t tile, uint32_t stage_lo, uint32_t stage_hi,
+    uint32_t first_step, SortBin bin) {
   __shared__ uint2 s[kSortTile];
-  const uint32_t base = blockIdx.x * tile;
-  for (uint32_t q = threadIdx.x; q < tile; q += blockDim.x) s[q] = lookup[base + q];
+  const uint32_t base0 = blockIdx.x * tile;
+  for (uint32_t q = threadIdx.x; q < tile; q += blockDim.x) {
+    const uint32_t gq = base0 + q;
+    s[q] = (BIN && gq < bin.n) ? bin_entry(bin, gq) : lookup[gq];
+  }
   __syncthreads();
   for (uint32_t stage = stage_lo; stage <= stage_hi; ++stage) {
-    for (uint32_t step = (stage == stage_lo ? first_step : 0u); step <= stage; ++step) {
-      const uint32_t gw = 1u << (stage - step);
-      for (uint32_t i = threadIdx.x; i < tile / 2u; i += blockDim.x) {
-        uint32_t l, r;
-        bitonic_pair(i, gw, step == 0u, l, r);
-        const uint2 a = s[l], b = s[r];
-        if (a.x > b.x) {
-          s[l] = b;
-          s[r] = a;
+    uint32_t step = stage == stage_lo ? first_step : 0u;
+    while (step <= stage) {
+      const uint32_t G = 1u << (stage - step);
+      const uint32_t left = stage - step + 1u;  // passes left in this stage
+      // A flip pass with G = 1 pairs (2i, 2i+1) exactly like a non-flip one.
+      const bool flip = step == 0u && G > 1u;
+      const uint32_t kf = KMAX > 1 ? (uint32_t)KMAX - 1u : 1u;  // flip chunks: 2^(K+1) entries
+      const uint32_t K = flip ? (G >= (2u << (kf - 1u)) ? kf : 1u)
+                              : (left < (uint32_t)KMAX ? left : (uint32_t)KMAX);
+      const uint32_t g = G >> (K - 1u);
+      const uint32_t groups = sort_groups(tile, G, g, flip);
+      for (uint32_t q = threadIdx.x; q < groups; q += blockDim.x) {
+        uint32_t b, r;
+        sort_group_at(q, G, g, flip, b, r);
+        if (flip) {
+          if (KMAX >= 3 && K == 2u) sort_group<2, true>(s, b, r, g);
+          else sort_group<1, true>(s, b, r, g);
+        } else {
+          if (KMAX >= 3 && K == 3u) sort_group<3, false>(s, b, r, g);
+          else if (KMAX >= 2 && K == 2u) sort_group<2, false>(s, b, r, g);
+          else sort_group<1, false>(s, b, r, g);
         }
       }
       __syncthreads();
+      step += K;
     }
   }
-  for (uint32_t q = threadIdx.x; q < tile; q += blockDim.x) lookup[base + q] = s[q];
+  for (uint32_t q = threadIdx.x; q < tile; q += blockDim.x) lookup[base0 + q] = s[q];
 }
 
 // calculate_spatial_lookup_offsets, compute_shader.wgsl:507-525.
@@ -631,49 +707,34 @@ __global__ __launch_bounds__(kBlock) void sph_offsets_kernel(const uint2* __rest
   if (key != prev) offsets[key] = i;
 }
 
-// pre_simulation_step part 1 (wgsl:397-405): gravity + predicted position for all
-// particles, so the density pass reads a complete snapshot.
-__global__ __launch_bounds__(kBlock) void sph_predict_kernel(const rps_config* __restrict__ cfg,
-                                                             const float* __restrict__ x,
-                                                             const float* __restrict__ y,
-                                                             float* __restrict__ vx,
-                                                             float* __restrict__ vy,
-                                                             f2* __restrict__ pred, uint32_t n) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  const float dt = cfg->fixed_delta_time;
-  const float qx = vx[i] + 0.0f * dt;
-  const float qy = vy[i] + (-cfg->gravity) * dt;
-  vx[i] = qx;
-  vy[i] = qy;
-  pred[i] = f2{x[i] + qx * dt, y[i] + qy * dt};
-}
-
 __constant__ int32_t kGridOff[9][2] = {{-1, -1}, {-1, 0}, {-1, 1}, {0, -1}, {0, 0},
                                        {0, 1},   {1, -1}, {1, 0},  {1, 1}};
 
-// Neighbour data in lookup order: entry j <- particle lookup[j].y (wgsl:239-240, :313-314,
-// :371 read exactly these values, pads included).
-__global__ __launch_bounds__(kBlock) void sph_gather_pv_kernel(const uint2* __restrict__ lookup,
-                                                               const f2* __restrict__ pred,
-                                                               const float* __restrict__ vx,
-                                                               const float* __restrict__ vy,
-                                                               f2* __restrict__ pred_s,
-                                                               f2* __restrict__ vel_s, uint32_t n) {
-  const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
-  if (j >= n) return;
-  const uint32_t i = lookup[j].y;
-  pred_s[j] = pred[i];
-  vel_s[j] = f2{vx[i], vy[i]};
-}
-
-__global__ __launch_bounds__(kBlock) void sph_gather_dens_kernel(const uint2* __restrict__ lookup,
-                                                                 const f2* __restrict__ dens,
-                                                                 f2* __restrict__ dens_s,
-                                                                 uint32_t n) {
-  const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
-  if (j >= n) return;
-  dens_s[j] = dens[lookup[j].y];
+// pre_simulation_step part 1 (wgsl:397-405) in lookup order: slot t (of all P) takes
+// particle i = lookup[t].y, applies gravity and predicts, and writes the results to slot t
+// (vel_s, pred_s) and pred[i].  The density and sim passes then read a complete snapshot
+// (DESIGN.md §3.3), a cell's entries contiguously, and their own particle at their own slot.
+// Pad slots repeat some particle and write identical values.
+__global__ __launch_bounds__(kBlock) void sph_predict_kernel(const rps_config* __restrict__ cfg,
+                                                             const uint2* __restrict__ lookup,
+                                                             const float* __restrict__ x,
+                                                             const float* __restrict__ y,
+                                                             const float* __restrict__ vx,
+                                                             const float* __restrict__ vy,
+                                                             f2* __restrict__ pred,
+                                                             f2* __restrict__ pred_s,
+                                                             f2* __restrict__ vel_s,
+                                                             uint32_t p_slots) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= p_slots) return;
+  const uint32_t i = lookup[t].y;
+  const float dt = cfg->fixed_delta_time;
+  const float qx = vx[i] + 0.0f * dt;  // apply_gravity, wgsl:397-400
+  const float qy = vy[i] + (-cfg->gravity) * dt;
+  const f2 p = f2{x[i] + qx * dt, y[i] + qy * dt};  // wgsl:402-405
+  vel_s[t] = f2{qx, qy};
+  pred_s[t] = p;
+  pred[i] = p;
 }
 
 constexpr int kScanBatch = 4;  // lookup entries in flight per lane in the neighbour scans
@@ -693,16 +754,17 @@ __device__ __forceinline__ uint32_t grid_key(int32_t cx, int32_t cy, int o, uint
 __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* __restrict__ cfg,
                                                              const uint2* __restrict__ lookup,
                                                              const uint32_t* __restrict__ offsets,
-                                                             const f2* __restrict__ pred,
                                                              const f2* __restrict__ pred_s,
-                                                             f2* __restrict__ dens, uint32_t p_slots) {
+                                                             f2* __restrict__ dens,
+                                                             f2* __restrict__ dens_s,
+                                                             uint32_t p_slots) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= p_slots) return;
   const uint32_t i = lookup[t].y;
   const float r = cfg->smoothing_radius, r2 = r * r;
   const uint32_t N = cfg->particle_count;
   const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
-  const f2 p = pred[i];
+  const f2 p = pred_s[t];
   const int32_t cx = f32_to_i32((p[0] + cfg->screen_bounds[1]) / r);
   const int32_t cy = f32_to_i32((p[1] + cfg->screen_bounds[3]) / r);
   float d = 0.0f, nd = 0.0f;
@@ -744,6 +806,7 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
     }
   }
   dens[i] = f2{d, nd};
+  dens_s[t] = f2{d, nd};
 }
 
 // simulation_step, compute_shader.wgsl:435-453: pressure (:256-334) and viscosity
@@ -752,13 +815,9 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
 __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __restrict__ cfg,
                                                          const uint2* __restrict__ lookup,
                                                          const uint32_t* __restrict__ offsets,
-                                                         const f2* __restrict__ pred,
-                                                         const f2* __restrict__ dens,
                                                          const f2* __restrict__ pred_s,
                                                          const f2* __restrict__ dens_s,
                                                          const f2* __restrict__ vel_s,
-                                                         const float* __restrict__ vx,
-                                                         const float* __restrict__ vy,
                                                          const float* __restrict__ x,
                                                          const float* __restrict__ y,
                                                          float* __restrict__ vx2,
@@ -775,10 +834,10 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
   const float nm = cfg->near_density_multiplier;
   const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
   const float vn = cfg->viscocity_kernel_norm;
-  const f2 p = pred[i];
+  const f2 p = pred_s[t];
   const int32_t cx = f32_to_i32((p[0] + cfg->screen_bounds[1]) / r);
   const int32_t cy = f32_to_i32((p[1] + cfg->screen_bounds[3]) / r);
-  const f2 rr = dens[i];
+  const f2 rr = dens_s[t];
   const float rho = rr[0], rhon = rr[1];
   const float P = (rho - td) * pm;
   const float Pn = rhon * nm;
@@ -838,8 +897,9 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
       if (stop) break;
     }
   }
-  float qx = vx[i] + fx * dt;
-  float qy = vy[i] + fy * dt;
+  const f2 own_v = vel_s[t];  // post-gravity velocity (the pre pass, wgsl:397-400)
+  float qx = own_v[0] + fx * dt;
+  float qy = own_v[1] + fy * dt;
   float wx = 0.0f, wy = 0.0f;
   for (int o = 0; o < 9; ++o) {
     const uint32_t key = grid_key(cx, cy, o, N);
@@ -1082,12 +1142,40 @@ hipError_t launch_nbody_integrate(const NbodyIntegrateArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_sph_bin(const SphBuffers& b, hipStream_t s) {
-  hipLaunchKernelGGL(sph_bin_kernel, dim3(blocks_for(b.n)), dim3(kBlock), 0, s, b.cfg, b.x, b.y,
-                     b.lookup, b.offsets, b.n);
+
+// Launch K global passes of one stage starting at stride G (flip = it is the stage's first).
+template <int K>
+static hipError_t launch_sort_fused(uint2* lookup, uint32_t P, uint32_t G, bool flip, hipStream_t s) {
+  const uint32_t g = G >> (K - 1);
+  const uint32_t threads = (P / (2u * G)) * (flip ? g / 2u : g);
+  if (flip)
+    hipLaunchKernelGGL((sph_sort_fused_kernel<K, true>), dim3(blocks_for(threads)), dim3(kBlock), 0, s,
+                       lookup, P, G);
+  else
+    hipLaunchKernelGGL((sph_sort_fused_kernel<K, false>), dim3(blocks_for(threads)), dim3(kBlock), 0, s,
+                       lookup, P, G);
   return hipGetLastError();
 }
 
+static hipError_t launch_sort_local(int kmax, bool bin, uint32_t tiles, uint32_t threads,
+                                    hipStream_t s, uint2* lookup, uint32_t tile, uint32_t lo,
+                                    uint32_t hi, uint32_t first, const SortBin& sb) {
+#define RPS_LOCAL(B, K) \
+  hipLaunchKernelGGL((sph_sort_local_kernel<B, K>), dim3(tiles), dim3(threads), 0, s, lookup, tile, lo, hi, first, sb)
+  if (bin) {
+    if (kmax == 3) RPS_LOCAL(true, 3);
+    else if (kmax == 2) RPS_LOCAL(true, 2);
+    else RPS_LOCAL(true, 1);
+  } else {
+    if (kmax == 3) RPS_LOCAL(false, 3);
+    else if (kmax == 2) RPS_LOCAL(false, 2);
+    else RPS_LOCAL(false, 1);
+  }
+#undef RPS_LOCAL
+  return hipGetLastError();
+}
+
+// Passes 1-2 of the frame: bin (folded into the first sort launch) + the bitonic network.
 hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
                            uint32_t* launches) {
   const uint32_t P = b.p;
@@ -1095,39 +1183,56 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
   while ((1u << stages) < P) ++stages;
   *passes = stages * (stages + 1u) / 2u;
   *launches = 0;
-  if (stages == 0) return hipSuccess;
+  static const int kmax = [] {
+    const char* v = std::getenv("RPS_SORT_KMAX");
+    const int k = v && *v ? std::atoi(v) : 2;  // measured best
+    return k < 1 ? 1 : (k > 3 ? 3 : k);
+  }();
+  const SortBin bin{b.cfg, b.x, b.y, b.offsets, b.n};
+  const SortBin nobin{nullptr, nullptr, nullptr, nullptr, 0u};
+  if (stages == 0) {  // P == 1: nothing to sort, only bin
+    hipLaunchKernelGGL((sph_sort_local_kernel<true, 1>), dim3(1), dim3(64), 0, s, b.lookup, 1u, 1u, 0u,
+                       0u, bin);
+    ++*launches;
+    return hipGetLastError();
+  }
   // Tile: 2048 entries up to P = 2^18 (enough workgroups to fill the chip in the LDS
   // passes), 8192 above (fewer global passes; measured at 50 k / 1 M / 4 M particles).
   const uint32_t want = P <= (1u << 18) ? 2048u : kSortTile;
   const uint32_t tile = P < want ? P : want;
   uint32_t tile_log = 0;
   while ((1u << tile_log) < tile) ++tile_log;
-  const uint32_t local_threads = tile / 2u < 1024u ? tile / 2u : 1024u;
   const uint32_t tiles = P / tile;
-  // Stages whose whole network fits one tile: one launch.
+  // Stages whose whole network fits one tile: one launch (with the bin pass).
   const uint32_t first_global_stage = tile_log;  // stage s has 2*2^s = 2^(s+1) span
-  hipLaunchKernelGGL(sph_sort_local_kernel, dim3(tiles), dim3(local_threads), 0, s, b.lookup,
-                     tile, 0u, first_global_stage - 1u, 0u);
+  const uint32_t lt = std::max(64u, std::min(1024u, tile >> kmax));
+  hipError_t e = launch_sort_local(kmax, true, tiles, lt, s, b.lookup, tile, 0u, first_global_stage - 1u,
+                                   0u, bin);
   ++*launches;
-  hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   for (uint32_t stage = first_global_stage; stage < stages; ++stage) {
+    // Passes whose compare span 2*gw exceeds the tile are global: steps [0, T).  They run
+    // in register-fused chunks of up to kSortFuse passes (sph_sort_fused_kernel).
+    uint32_t T = 0;
+    while (T <= stage && 2u * (1u << (stage - T)) > tile) ++T;
     uint32_t step = 0;
-    // Passes whose compare span 2*gw exceeds the tile run as global passes.
-    for (; step <= stage; ++step) {
-      const uint32_t gw = 1u << (stage - step);
-      if (2u * gw <= tile) break;
-      hipLaunchKernelGGL(sph_sort_global_kernel, dim3(blocks_for(P / 2u)), dim3(kBlock), 0, s,
-                         b.lookup, P, gw, step == 0u ? 1u : 0u);
+    while (step < T) {
+      const uint32_t k = T - step < kSortFuse ? T - step : kSortFuse;
+      const uint32_t G = 1u << (stage - step);
+      const bool flip = step == 0;
+      switch (k) {
+        case 1: e = launch_sort_fused<1>(b.lookup, P, G, flip, s); break;
+        case 2: e = launch_sort_fused<2>(b.lookup, P, G, flip, s); break;
+        case 3: e = launch_sort_fused<3>(b.lookup, P, G, flip, s); break;
+        default: e = launch_sort_fused<4>(b.lookup, P, G, flip, s); break;
+      }
       ++*launches;
-      e = hipGetLastError();
       if (e != hipSuccess) return e;
+      step += k;
     }
     if (step <= stage) {
-      hipLaunchKernelGGL(sph_sort_local_kernel, dim3(tiles), dim3(local_threads), 0, s, b.lookup,
-                         tile, stage, stage, step);
+      e = launch_sort_local(kmax, false, tiles, lt, s, b.lookup, tile, stage, stage, step, nobin);
       ++*launches;
-      e = hipGetLastError();
       if (e != hipSuccess) return e;
     }
   }
@@ -1141,27 +1246,18 @@ hipError_t launch_sph_offsets(const SphBuffers& b, hipStream_t s) {
 }
 
 hipError_t launch_sph_pre(const SphBuffers& b, hipStream_t s) {
-  hipLaunchKernelGGL(sph_predict_kernel, dim3(blocks_for(b.n)), dim3(kBlock), 0, s, b.cfg, b.x,
-                     b.y, b.vx, b.vy, b.pred, b.n);
+  hipLaunchKernelGGL(sph_predict_kernel, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg, b.lookup,
+                     b.x, b.y, b.vx, b.vy, b.pred, b.pred_s, b.vel_s, b.p);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(sph_gather_pv_kernel, dim3(blocks_for(b.n)), dim3(kBlock), 0, s, b.lookup,
-                     b.pred, b.vx, b.vy, b.pred_s, b.vel_s, b.n);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(sph_density_kernel, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg,
-                     b.lookup, b.offsets, b.pred, b.pred_s, b.dens, b.p);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(sph_gather_dens_kernel, dim3(blocks_for(b.n)), dim3(kBlock), 0, s, b.lookup,
-                     b.dens, b.dens_s, b.n);
+                     b.lookup, b.offsets, b.pred_s, b.dens, b.dens_s, b.p);
   return hipGetLastError();
 }
 
 hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s) {
   hipLaunchKernelGGL(sph_sim_kernel, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg, b.lookup,
-                     b.offsets, b.pred, b.dens, b.pred_s, b.dens_s, b.vel_s, b.vx, b.vy, b.x, b.y,
-                     b.vx2, b.vy2, b.x2, b.y2, b.p);
+                     b.offsets, b.pred_s, b.dens_s, b.vel_s, b.x, b.y, b.vx2, b.vy2, b.x2, b.y2, b.p);
   return hipGetLastError();
 }
 

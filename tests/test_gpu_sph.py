@@ -76,3 +76,23 @@ def test_sph_config_validation(gpu):
         with pytest.raises(rps.RpsError) as e:
             ctx.set_config(rps.default_particle_config(128), rps.headline_ext())
         assert e.value.status == rps.RPS_ERR_UNSUPPORTED
+
+
+@pytest.mark.parametrize("n", [(1 << 20) + 5, 300000])
+def test_sph_grid_passes_large(gpu, orc, n):
+    """bin + bitonic + offsets at P = 2^21 / 2^19 (8192-entry LDS tiles, register-fused global
+    passes of up to 4 network steps) against the oracle's pass-per-dispatch network; passes
+    4-5 gated off (shader_delay) so only the integer passes run."""
+    rps = gpu
+    cfg = rps.default_particle_config(n, gravity=100.0)
+    soa = _blob(n, 7, spread=300.0)
+    ext = rps.make_ext(shader_delay=100)
+    st = orc.SphState(n)
+    ref = copy_soa(soa)
+    with rps.Context(n, rps.MODE_SPH) as ctx:
+        ctx.set_config(cfg, ext)
+        ctx.upload_soa(soa)
+        ctx.step(1)
+        st.grid(cfg, ref)
+        assert_bitwise(ctx.read_debug(rps.DEBUG_SPATIAL_LOOKUP), st.lookup, "lookup")
+        assert_bitwise(ctx.read_debug(rps.DEBUG_LOOKUP_OFFSETS), st.offsets, "offsets")
