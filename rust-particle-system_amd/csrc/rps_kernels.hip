@@ -744,6 +744,17 @@ __device__ __forceinline__ uint32_t grid_key(int32_t cx, int32_t cy, int o, uint
                   (int32_t)((uint32_t)cy + (uint32_t)kGridOff[o][1]), N);
 }
 
+// The 3x3 cells around (cx, cy) in the reference's order (wgsl:223-224 / :277-278): their
+// keys and first lookup slots, the nine offsets loads issued together.
+__device__ __forceinline__ void cell_starts(const uint32_t* __restrict__ offsets, int32_t cx,
+                                            int32_t cy, uint32_t N, uint32_t keys[9],
+                                            uint32_t starts[9]) {
+#pragma unroll
+  for (int o = 0; o < 9; ++o) keys[o] = grid_key(cx, cy, o, N);
+#pragma unroll
+  for (int o = 0; o < 9; ++o) starts[o] = offsets[keys[o]];
+}
+
 // Work mapping of the density and sim passes: thread t takes the particle in lookup slot t,
 // t in [0, P).  Lanes of a wave then hold spatially adjacent particles and scan the same
 // cells.  Every particle's fresh entry is in exactly one slot; pad slots
@@ -767,10 +778,12 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
   const f2 p = pred_s[t];
   const int32_t cx = f32_to_i32((p[0] + cfg->screen_bounds[1]) / r);
   const int32_t cy = f32_to_i32((p[1] + cfg->screen_bounds[3]) / r);
+  uint32_t keys[9], starts[9];
+  cell_starts(offsets, cx, cy, N, keys, starts);
   float d = 0.0f, nd = 0.0f;
   for (int o = 0; o < 9; ++o) {
-    const uint32_t key = grid_key(cx, cy, o, N);
-    for (uint32_t j = offsets[key]; j < N; j += kScanBatch) {
+    const uint32_t key = keys[o];
+    for (uint32_t j = starts[o]; j < N; j += kScanBatch) {
       uint32_t k[kScanBatch];
       f2 q[kScanBatch];
 #pragma unroll
@@ -843,10 +856,12 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
   const float Pn = rhon * nm;
   const float P_rho2 = P / (rho * rho);    // loop-invariant halves of pressure_term and
   const float Pn_rho2 = Pn / (rho * rho);  // near_pressure_term (wgsl:323-327)
+  uint32_t keys[9], starts[9];
+  cell_starts(offsets, cx, cy, N, keys, starts);
   float fx = 0.0f, fy = 0.0f;
   for (int o = 0; o < 9; ++o) {
-    const uint32_t key = grid_key(cx, cy, o, N);
-    for (uint32_t j = offsets[key]; j < N; j += kScanBatch) {
+    const uint32_t key = keys[o];
+    for (uint32_t j = starts[o]; j < N; j += kScanBatch) {
       uint2 e[kScanBatch];
       f2 q[kScanBatch], dj[kScanBatch];
 #pragma unroll
@@ -902,8 +917,8 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
   float qy = own_v[1] + fy * dt;
   float wx = 0.0f, wy = 0.0f;
   for (int o = 0; o < 9; ++o) {
-    const uint32_t key = grid_key(cx, cy, o, N);
-    for (uint32_t j = offsets[key]; j < N; j += kScanBatch) {
+    const uint32_t key = keys[o];
+    for (uint32_t j = starts[o]; j < N; j += kScanBatch) {
       uint2 e[kScanBatch];
       f2 q[kScanBatch], vj[kScanBatch];
 #pragma unroll

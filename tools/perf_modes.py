@@ -37,7 +37,7 @@ def sph(n, frames=50):
     out[f"sph_{n}"] = r
 
 
-def nbody(n, steps=3):
+def nbody(n, steps=3, warm=1):
     cfg = rps.default_particle_config(n, gravity=0.0)
     ext = rps.make_ext(nbody_strength=1.0, nbody_softening=1.0, shader_delay=0)
     g = np.random.default_rng(0)
@@ -46,7 +46,7 @@ def nbody(n, steps=3):
     with rps.Context(n, rps.MODE_NBODY) as ctx:
         ctx.set_config(cfg, ext)
         ctx.upload_soa(soa)
-        ctx.step(1)
+        ctx.step(warm)
         ctx.sync()
         ctx.set_profiling(1)
         ctx.step(steps)
@@ -122,6 +122,9 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "sph":
         for n in (50000, 65536, 1 << 20, 1 << 22):
             sph(n)
+        sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "c4":  # BASELINE configs[3]: 2^24 all-pairs, one step
+        nbody(1 << 24, steps=1, warm=0)
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "nbody":
         for n in (1 << 16, 1 << 17, 1 << 18, 1 << 20):
