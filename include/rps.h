@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RPS_ABI_VERSION 1u
+#define RPS_ABI_VERSION 2u  /* 2: lifetime kept as an expiry (RPS_FIELD_LIFE_STEPS, RPS_DEBUG_EXPIRY) */
 
 /* ------------------------------------------------------------------------------------ */
 /* Status codes                                                                          */

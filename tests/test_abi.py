@@ -66,7 +66,7 @@ def test_c_header_compiles_and_sizes_agree(tmp_path):
 
 def test_status_strings_and_null_handling(rps):
     L = rps.lib()
-    assert L.rps_abi_version() == 1
+    assert L.rps_abi_version() == 2
     assert L.rps_status_string(0) == b"ok"
     assert L.rps_status_string(4) == b"unsupported"
     # null arguments are rejected without touching the device
