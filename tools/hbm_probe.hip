@@ -173,6 +173,39 @@ __global__ __launch_bounds__(256) void rmw4e_k(f4* base, size_t n4, float s, uns
   __builtin_nontemporal_store(D * s + A, t + 3 * T4);
 }
 
+// Tiled, every store depending on its own load only (as flat_rmw_u).
+template <int T>
+__global__ __launch_bounds__(256) void rmw5_tiled_indep_k(f4* base, size_t n4, float s) {
+  size_t v = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= n4) return;
+  constexpr size_t T4 = T / 4;
+  const size_t tile = v / T4, w = v % T4;
+  f4* t = base + tile * 5 * T4 + w;
+  f4 A = ld<true>(t), B = ld<true>(t + T4), C = ld<true>(t + 2 * T4), D = ld<true>(t + 3 * T4), E = ld<true>(t + 4 * T4);
+  st<true>(t, A * s + 1.0f);
+  st<true>(t + T4, B * s + 1.0f);
+  st<true>(t + 2 * T4, C * s + 1.0f);
+  st<true>(t + 3 * T4, D * s + 1.0f);
+  st<true>(t + 4 * T4, E * s + 1.0f);
+}
+
+// Tiled with all stores depending on all loads (the particle step's shape).
+template <int T>
+__global__ __launch_bounds__(256) void rmw5_tiled_all_k(f4* base, size_t n4, float s) {
+  size_t v = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= n4) return;
+  constexpr size_t T4 = T / 4;
+  const size_t tile = v / T4, w = v % T4;
+  f4* t = base + tile * 5 * T4 + w;
+  f4 A = ld<true>(t), B = ld<true>(t + T4), C = ld<true>(t + 2 * T4), D = ld<true>(t + 3 * T4), E = ld<true>(t + 4 * T4);
+  const f4 S = (A + B) + (C + D) + E;
+  st<true>(t, A * s + S);
+  st<true>(t + T4, B * s + S);
+  st<true>(t + 2 * T4, C * s + S);
+  st<true>(t + 3 * T4, D * s + S);
+  st<true>(t + 4 * T4, E * s + S);
+}
+
 // Same with 512-thread workgroups.
 template <bool NT, int T>
 __global__ __launch_bounds__(512) void rmw5_tiled_b512_k(f4* base, size_t n4, float s) {
@@ -282,6 +315,11 @@ int main(int argc, char** argv) {
     run("flat rmw u5", 40.0 * n, [&] { hipLaunchKernelGGL((flat_rmw_u_k<true, 5>), dim3((gf + 4) / 5), dim3(256), 0, 0, tb, f4n, 1.0f); });
     run("flat rmw u4", 40.0 * n, [&] { hipLaunchKernelGGL((flat_rmw_u_k<true, 4>), dim3((gf + 3) / 4), dim3(256), 0, 0, tb, f4n, 1.0f); });
     run("flat copy", 40.0 * n, [&] { hipLaunchKernelGGL(copy_k<true>, dim3(gf), dim3(256), 0, 0, tb, tb2, f4n); std::swap(tb, tb2); });
+    run("t1024 indep", 40.0 * n, [&] { hipLaunchKernelGGL((rmw5_tiled_indep_k<1024>), dim3(g), dim3(256), 0, 0, tb, n4, 1.0f); });
+    run("t8192 indep", 40.0 * n, [&] { hipLaunchKernelGGL((rmw5_tiled_indep_k<8192>), dim3(g), dim3(256), 0, 0, tb, n4, 1.0f); });
+    run("t1024 all", 40.0 * n, [&] { hipLaunchKernelGGL((rmw5_tiled_all_k<1024>), dim3(g), dim3(256), 0, 0, tb, n4, 1.0f); });
+    run("t8192 all", 40.0 * n, [&] { hipLaunchKernelGGL((rmw5_tiled_all_k<8192>), dim3(g), dim3(256), 0, 0, tb, n4, 1.0f); });
+    run("t1024 nt", 40.0 * n, [&] { hipLaunchKernelGGL((rmw5_tiled_k<true, 1024>), dim3(g), dim3(256), 0, 0, tb, n4, 1.0f); });
     run("t8192 4f+u16", 34.0 * n, [&] { hipLaunchKernelGGL((rmw4e_k<8192, true>), dim3(g), dim3(256), 0, 0, tb, n4, 1.0f, (unsigned short)7); });
     run("t8192 4f", 32.0 * n, [&] { hipLaunchKernelGGL((rmw4e_k<8192, false>), dim3(g), dim3(256), 0, 0, tb, n4, 1.0f, (unsigned short)7); });
     run("t4096 4f+u16", 34.0 * n, [&] { hipLaunchKernelGGL((rmw4e_k<4096, true>), dim3(g), dim3(256), 0, 0, tb, n4, 1.0f, (unsigned short)7); });
