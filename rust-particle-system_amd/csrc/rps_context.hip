@@ -42,7 +42,8 @@ struct rps_ctx {
   uint16_t* exp = nullptr;         // STREAM: lifetime expiry (u16)
   // SPH
   float *vx2 = nullptr, *vy2 = nullptr, *x2 = nullptr, *y2 = nullptr;
-  f2 *pred_s = nullptr, *vel_s = nullptr, *dens_s = nullptr;
+  uint4* rec_s = nullptr;  // SPH slot records (rps_internal.hpp SphBuffers)
+  f4* dv_s = nullptr;
   uint2* lookup = nullptr;
   uint32_t* offsets = nullptr;
   f2* dens = nullptr;
@@ -257,9 +258,8 @@ SphBuffers sph_buffers(rps_ctx* ctx) {
   b.vy2 = ctx->vy2;
   b.x2 = ctx->x2;
   b.y2 = ctx->y2;
-  b.pred_s = ctx->pred_s;
-  b.vel_s = ctx->vel_s;
-  b.dens_s = ctx->dens_s;
+  b.rec_s = ctx->rec_s;
+  b.dv_s = ctx->dv_s;
   b.lookup = ctx->lookup;
   b.offsets = ctx->offsets;
   b.dens = ctx->dens;
@@ -509,9 +509,8 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     slots.push_back({(void**)&ctx->vy2, nf});
     slots.push_back({(void**)&ctx->x2, nf});
     slots.push_back({(void**)&ctx->y2, nf});
-    slots.push_back({(void**)&ctx->pred_s, align_up((size_t)ctx->P * sizeof(f2), 256)});
-    slots.push_back({(void**)&ctx->vel_s, align_up((size_t)ctx->P * sizeof(f2), 256)});
-    slots.push_back({(void**)&ctx->dens_s, align_up((size_t)ctx->P * sizeof(f2), 256)});
+    slots.push_back({(void**)&ctx->rec_s, align_up((size_t)ctx->P * sizeof(uint4), 256)});
+    slots.push_back({(void**)&ctx->dv_s, align_up((size_t)ctx->P * sizeof(f4), 256)});
     slots.push_back({(void**)&ctx->lookup, align_up((size_t)ctx->P * sizeof(uint2), 256)});
     slots.push_back({(void**)&ctx->offsets, align_up(n * sizeof(uint32_t), 256)});
     slots.push_back({(void**)&ctx->dens, align_up(n * sizeof(f2), 256)});

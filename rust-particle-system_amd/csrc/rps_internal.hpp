@@ -96,12 +96,11 @@ struct SphBuffers {
   uint32_t* offsets; // N
   f2* dens;          // N
   f2* pred;          // N
-  // Neighbour data gathered into spatial-lookup order (entry j holds particle lookup[j].y's
-  // value), so a cell's entries are contiguous: pred_s/vel_s after prediction, dens_s after
-  // the density pass.
-  f2* pred_s;        // P (every lookup slot)
-  f2* vel_s;         // P
-  f2* dens_s;        // P
+  // Neighbour data in spatial-lookup order (slot j holds particle lookup[j].y's values), so
+  // a cell's entries are contiguous: rec_s and dv_s.zw after prediction, dv_s.xy after the
+  // density pass.
+  uint4* rec_s;      // P slot records {key, index, predicted x, y}
+  f4* dv_s;          // P {density, near density, post-gravity vx, vy}
   uint32_t n;        // N
   uint32_t p;        // next_pow2(N)
 };

@@ -712,8 +712,10 @@ __constant__ int32_t kGridOff[9][2] = {{-1, -1}, {-1, 0}, {-1, 1}, {0, -1}, {0, 
 
 // pre_simulation_step part 1 (wgsl:397-405) in lookup order: slot t (of all P) takes
 // particle i = lookup[t].y, applies gravity and predicts, and writes the results to slot t
-// (vel_s, pred_s) and pred[i].  The density and sim passes then read a complete snapshot
-// (DESIGN.md §3.3), a cell's entries contiguously, and their own particle at their own slot.
+// and pred[i]: the slot record rec_s[t] = {key, i, predicted x, y} and dv_s[t].zw = the
+// post-gravity velocity (dv_s[t].xy gets the densities in the density pass).  The density
+// and sim passes then read a complete snapshot, a cell's entries
+// contiguously with one 16-B load per record, and their own particle at their own slot.
 // Pad slots repeat some particle and write identical values.
 __global__ __launch_bounds__(kBlock) void sph_predict_kernel(const rps_config* __restrict__ cfg,
                                                              const uint2* __restrict__ lookup,
@@ -722,22 +724,23 @@ __global__ __launch_bounds__(kBlock) void sph_predict_kernel(const rps_config* _
                                                              const float* __restrict__ vx,
                                                              const float* __restrict__ vy,
                                                              f2* __restrict__ pred,
-                                                             f2* __restrict__ pred_s,
-                                                             f2* __restrict__ vel_s,
+                                                             uint4* __restrict__ rec_s,
+                                                             f4* __restrict__ dv_s,
                                                              uint32_t p_slots) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= p_slots) return;
-  const uint32_t i = lookup[t].y;
+  const uint2 e = lookup[t];
+  const uint32_t i = e.y;
   const float dt = cfg->fixed_delta_time;
   const float qx = vx[i] + 0.0f * dt;  // apply_gravity, wgsl:397-400
   const float qy = vy[i] + (-cfg->gravity) * dt;
   const f2 p = f2{x[i] + qx * dt, y[i] + qy * dt};  // wgsl:402-405
-  vel_s[t] = f2{qx, qy};
-  pred_s[t] = p;
+  rec_s[t] = make_uint4(e.x, i, __float_as_uint(p[0]), __float_as_uint(p[1]));
+  reinterpret_cast<f2*>(dv_s)[2 * t + 1] = f2{qx, qy};
   pred[i] = p;
 }
 
-constexpr int kScanBatch = 4;  // lookup entries in flight per lane in the neighbour scans
+// kScanBatch: lookup entries in flight per lane in the neighbour scans (template).
 
 __device__ __forceinline__ uint32_t grid_key(int32_t cx, int32_t cy, int o, uint32_t N) {
   return cell_key((int32_t)((uint32_t)cx + (uint32_t)kGridOff[o][0]),
@@ -762,20 +765,21 @@ __device__ __forceinline__ void cell_starts(const uint32_t* __restrict__ offsets
 // separate buffers), so the race is benign and results are independent of it.
 //
 // calculate_density, compute_shader.wgsl:207-254, entries summed in lookup order.
+template <int kScanBatch>
 __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* __restrict__ cfg,
-                                                             const uint2* __restrict__ lookup,
                                                              const uint32_t* __restrict__ offsets,
-                                                             const f2* __restrict__ pred_s,
+                                                             const uint4* __restrict__ rec_s,
                                                              f2* __restrict__ dens,
-                                                             f2* __restrict__ dens_s,
+                                                             f4* __restrict__ dv_s,
                                                              uint32_t p_slots) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= p_slots) return;
-  const uint32_t i = lookup[t].y;
+  const uint4 own = rec_s[t];
+  const uint32_t i = own.y;
   const float r = cfg->smoothing_radius, r2 = r * r;
   const uint32_t N = cfg->particle_count;
   const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
-  const f2 p = pred_s[t];
+  const f2 p = f2{__uint_as_float(own.z), __uint_as_float(own.w)};
   const int32_t cx = f32_to_i32((p[0] + cfg->screen_bounds[1]) / r);
   const int32_t cy = f32_to_i32((p[1] + cfg->screen_bounds[3]) / r);
   uint32_t keys[9], starts[9];
@@ -784,22 +788,17 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
   for (int o = 0; o < 9; ++o) {
     const uint32_t key = keys[o];
     for (uint32_t j = starts[o]; j < N; j += kScanBatch) {
-      uint32_t k[kScanBatch];
-      f2 q[kScanBatch];
+      uint4 e[kScanBatch];
 #pragma unroll
-      for (int u = 0; u < kScanBatch; ++u) {
-        const uint32_t jj = min(j + u, N - 1u);
-        k[u] = lookup[jj].x;
-        q[u] = pred_s[jj];
-      }
+      for (int u = 0; u < kScanBatch; ++u) e[u] = rec_s[min(j + u, N - 1u)];
       bool stop = false;
 #pragma unroll
       for (int u = 0; u < kScanBatch; ++u) {
         if (!stop) {
-          if (j + u >= N || k[u] != key) {
+          if (j + u >= N || e[u].x != key) {
             stop = true;
           } else {
-            const float dx = p[0] - q[u][0], dy = p[1] - q[u][1];
+            const float dx = p[0] - __uint_as_float(e[u].z), dy = p[1] - __uint_as_float(e[u].w);
             const float sq = dx * dx + dy * dy;
             if (!(sq > r2)) {
               const float dist = sqrtf(sq);
@@ -819,18 +818,17 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
     }
   }
   dens[i] = f2{d, nd};
-  dens_s[t] = f2{d, nd};
+  reinterpret_cast<f2*>(dv_s)[2 * t] = f2{d, nd};
 }
 
 // simulation_step, compute_shader.wgsl:435-453: pressure (:256-334) and viscosity
 // (:336-384) against the start-of-pass velocity snapshot (vel_s), Euler (:392-395) and walls
 // (:69-99).  New velocities/positions go to (vx2, vy2, x2, y2).
+template <int kScanBatch>
 __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __restrict__ cfg,
-                                                         const uint2* __restrict__ lookup,
                                                          const uint32_t* __restrict__ offsets,
-                                                         const f2* __restrict__ pred_s,
-                                                         const f2* __restrict__ dens_s,
-                                                         const f2* __restrict__ vel_s,
+                                                         const uint4* __restrict__ rec_s,
+                                                         const f4* __restrict__ dv_s,
                                                          const float* __restrict__ x,
                                                          const float* __restrict__ y,
                                                          float* __restrict__ vx2,
@@ -839,7 +837,9 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
                                                          float* __restrict__ y2, uint32_t p_slots) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= p_slots) return;
-  const uint32_t i = lookup[t].y;
+  const uint4 own = rec_s[t];
+  const f4 own_dv = dv_s[t];  // own densities (xy) and post-gravity velocity (zw)
+  const uint32_t i = own.y;
   const float dt = cfg->fixed_delta_time;
   const float r = cfg->smoothing_radius, r2 = r * r;
   const uint32_t N = cfg->particle_count;
@@ -847,11 +847,10 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
   const float nm = cfg->near_density_multiplier;
   const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
   const float vn = cfg->viscocity_kernel_norm;
-  const f2 p = pred_s[t];
+  const f2 p = f2{__uint_as_float(own.z), __uint_as_float(own.w)};
   const int32_t cx = f32_to_i32((p[0] + cfg->screen_bounds[1]) / r);
   const int32_t cy = f32_to_i32((p[1] + cfg->screen_bounds[3]) / r);
-  const f2 rr = dens_s[t];
-  const float rho = rr[0], rhon = rr[1];
+  const float rho = own_dv[0], rhon = own_dv[1];
   const float P = (rho - td) * pm;
   const float Pn = rhon * nm;
   const float P_rho2 = P / (rho * rho);    // loop-invariant halves of pressure_term and
@@ -862,14 +861,13 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
   for (int o = 0; o < 9; ++o) {
     const uint32_t key = keys[o];
     for (uint32_t j = starts[o]; j < N; j += kScanBatch) {
-      uint2 e[kScanBatch];
-      f2 q[kScanBatch], dj[kScanBatch];
+      uint4 e[kScanBatch];
+      f2 dj[kScanBatch];
 #pragma unroll
       for (int u = 0; u < kScanBatch; ++u) {
         const uint32_t jj = min(j + u, N - 1u);
-        e[u] = lookup[jj];
-        q[u] = pred_s[jj];
-        dj[u] = dens_s[jj];
+        e[u] = rec_s[jj];
+        dj[u] = reinterpret_cast<const f2*>(dv_s)[2 * jj];
       }
       bool stop = false;
 #pragma unroll
@@ -878,7 +876,7 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
           if (j + u >= N || e[u].x != key) {
             stop = true;
           } else if (e[u].y != i) {
-            const float dx = q[u][0] - p[0], dy = q[u][1] - p[1];
+            const float dx = __uint_as_float(e[u].z) - p[0], dy = __uint_as_float(e[u].w) - p[1];
             const float sq = dx * dx + dy * dy;
             if (!(sq > r2)) {
               const float dist = sqrtf(sq);
@@ -912,21 +910,19 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
       if (stop) break;
     }
   }
-  const f2 own_v = vel_s[t];  // post-gravity velocity (the pre pass, wgsl:397-400)
-  float qx = own_v[0] + fx * dt;
-  float qy = own_v[1] + fy * dt;
+  float qx = own_dv[2] + fx * dt;  // post-gravity velocity (the pre pass, wgsl:397-400)
+  float qy = own_dv[3] + fy * dt;
   float wx = 0.0f, wy = 0.0f;
   for (int o = 0; o < 9; ++o) {
     const uint32_t key = keys[o];
     for (uint32_t j = starts[o]; j < N; j += kScanBatch) {
-      uint2 e[kScanBatch];
-      f2 q[kScanBatch], vj[kScanBatch];
+      uint4 e[kScanBatch];
+      f2 vj[kScanBatch];
 #pragma unroll
       for (int u = 0; u < kScanBatch; ++u) {
         const uint32_t jj = min(j + u, N - 1u);
-        e[u] = lookup[jj];
-        q[u] = pred_s[jj];
-        vj[u] = vel_s[jj];
+        e[u] = rec_s[jj];
+        vj[u] = reinterpret_cast<const f2*>(dv_s)[2 * jj + 1];
       }
       bool stop = false;
 #pragma unroll
@@ -935,7 +931,7 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
           if (j + u >= N || e[u].x != key) {
             stop = true;
           } else if (e[u].y != i) {
-            const float dx = p[0] - q[u][0], dy = p[1] - q[u][1];
+            const float dx = p[0] - __uint_as_float(e[u].z), dy = p[1] - __uint_as_float(e[u].w);
             const float sq = dx * dx + dy * dy;
             if (!(sq > r2)) {
               const float dist = sqrtf(sq);
@@ -1260,19 +1256,35 @@ hipError_t launch_sph_offsets(const SphBuffers& b, hipStream_t s) {
   return hipGetLastError();
 }
 
+static int sph_batch() {
+  static const int b = [] {
+    const char* v = std::getenv("RPS_SPH_BATCH");
+    return v && *v && std::atoi(v) == 8 ? 8 : 4;
+  }();
+  return b;
+}
+
 hipError_t launch_sph_pre(const SphBuffers& b, hipStream_t s) {
   hipLaunchKernelGGL(sph_predict_kernel, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg, b.lookup,
-                     b.x, b.y, b.vx, b.vy, b.pred, b.pred_s, b.vel_s, b.p);
+                     b.x, b.y, b.vx, b.vy, b.pred, b.rec_s, b.dv_s, b.p);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(sph_density_kernel, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg,
-                     b.lookup, b.offsets, b.pred_s, b.dens, b.dens_s, b.p);
+  if (sph_batch() == 8)
+    hipLaunchKernelGGL(sph_density_kernel<8>, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg,
+                       b.offsets, b.rec_s, b.dens, b.dv_s, b.p);
+  else
+    hipLaunchKernelGGL(sph_density_kernel<4>, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg,
+                       b.offsets, b.rec_s, b.dens, b.dv_s, b.p);
   return hipGetLastError();
 }
 
 hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s) {
-  hipLaunchKernelGGL(sph_sim_kernel, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg, b.lookup,
-                     b.offsets, b.pred_s, b.dens_s, b.vel_s, b.x, b.y, b.vx2, b.vy2, b.x2, b.y2, b.p);
+  if (sph_batch() == 8)
+    hipLaunchKernelGGL(sph_sim_kernel<8>, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg,
+                       b.offsets, b.rec_s, b.dv_s, b.x, b.y, b.vx2, b.vy2, b.x2, b.y2, b.p);
+  else
+    hipLaunchKernelGGL(sph_sim_kernel<4>, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg,
+                       b.offsets, b.rec_s, b.dv_s, b.x, b.y, b.vx2, b.vy2, b.x2, b.y2, b.p);
   return hipGetLastError();
 }
 
