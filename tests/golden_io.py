@@ -1,0 +1,25 @@
+"""Loading the committed golden fixtures (tests/golden/*.npz, made by make_golden.py)."""
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+STREAM = ("stream_c1_subset.npz", "stream_c2_verlet.npz", "stream_c3_features.npz")
+SPH = ("sph_n1000.npz", "sph_n2048.npz")
+NBODY = ("nbody_n1024.npz",)
+
+
+def load(name):
+    with np.load(os.path.join(GOLDEN, name), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def structs(rps, g):
+    """The fixture's ParticleConfig and ExtConfig, byte for byte."""
+    cfg = rps.ParticleConfig.from_buffer_copy(g["cfg"].tobytes())
+    ext = rps.ExtConfig.from_buffer_copy(g["ext"].tobytes())
+    return cfg, ext
+
+
+def inputs(g):
+    return {k[3:]: v.copy() for k, v in g.items() if k.startswith("in_")}
