@@ -115,7 +115,8 @@ typedef enum rps_integrator {
 
 enum {
   RPS_EXT_LIFETIME = 1u << 0, /* lifetime in whole steps; respawn at the emitter on expiry (below) */
-  RPS_EXT_STATS = 1u << 1     /* fuse bbox / kinetic-energy / respawn-count reductions into the step */
+  RPS_EXT_STATS = 1u << 1,    /* fuse bbox / kinetic-energy / respawn-count reductions into the step */
+  RPS_EXT_NBODY_EXTERNAL = 1u << 2 /* N-body shards: the caller exchanges the sources (rps_nbody_sources) */
 };
 
 typedef struct rps_ext_config {
@@ -264,6 +265,12 @@ int rps_step_cost(const rps_ctx* ctx, double* amount, int* unit);
 /* Multi-GPU (N-body mode only needs it): RCCL communicator over this rank's context.
  * unique_id is the 128-byte ncclUniqueId produced by rps_comm_unique_id on rank 0. */
 int rps_comm_unique_id(void* out128);
+/* N-body sources: the device array of float2 positions of ALL global particles (global_count
+ * entries; this shard's at [id_offset, id_offset + n)).  pack != 0 first writes this shard's
+ * current positions into it (and waits for that).  With RPS_EXT_NBODY_EXTERNAL set, rps_step
+ * skips its own pack + ncclAllGather and uses the array as the caller left it, so a host can
+ * exchange shards with any transport (peer copies, MPI, host staging). */
+int rps_nbody_sources(rps_ctx* ctx, int pack, void** sources, uint64_t* count);
 int rps_comm_init(rps_ctx* ctx, int rank, int nranks, const void* unique_id128);
 
 #ifdef __cplusplus

@@ -347,8 +347,11 @@ int step_stream_fused(rps_ctx* ctx, uint64_t k0, uint32_t m, bool stats, uint64_
 int step_nbody(rps_ctx* ctx) {
   const rps_config& c = ctx->cfg;
   const rps_ext_config& e = ctx->ext;
-  RPS_HIP(ctx, launch_nbody_pack(ctx->x, ctx->y, ctx->pos_all + ctx->id_offset, ctx->n, ctx->stream));
-  if (ctx->nranks > 1) {
+  const bool external = (e.flags & RPS_EXT_NBODY_EXTERNAL) != 0;
+  // External exchange: the caller packed (rps_nbody_pack) and filled the other shards.
+  if (!external)
+    RPS_HIP(ctx, launch_nbody_pack(ctx->x, ctx->y, ctx->pos_all + ctx->id_offset, ctx->n, ctx->stream));
+  if (ctx->nranks > 1 && !external) {
     // In-place all-gather of every rank's float2 positions over xGMI.
     ncclResult_t r = ncclAllGather(ctx->pos_all + ctx->id_offset, ctx->pos_all, ctx->n * 2,
                                    ncclFloat, ctx->comm, ctx->stream);
@@ -596,6 +599,8 @@ int rps_set_config(rps_ctx* ctx, const rps_config* cfg, const rps_ext_config* ex
   if (e.integrator > RPS_INTEGRATOR_VERLET) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "bad integrator");
   if (e.num_attractors > RPS_MAX_ATTRACTORS)
     return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "num_attractors > RPS_MAX_ATTRACTORS");
+  if ((e.flags & RPS_EXT_NBODY_EXTERNAL) && ctx->mode != RPS_MODE_NBODY)
+    return fail(ctx, RPS_ERR_UNSUPPORTED, "RPS_EXT_NBODY_EXTERNAL is an N-body flag");
   if (ctx->mode != RPS_MODE_STREAM && (e.flags & (RPS_EXT_LIFETIME | RPS_EXT_STATS)))
     return fail(ctx, RPS_ERR_UNSUPPORTED, "lifetime/stats extensions exist in STREAM mode only");
   if (ctx->mode != RPS_MODE_STREAM && (e.integrator != RPS_INTEGRATOR_EULER || e.num_attractors))
@@ -823,10 +828,11 @@ int rps_step(rps_ctx* ctx, uint32_t nsteps) {
   int rc = check_ctx(ctx);
   if (rc) return rc;
   if (!ctx->have_config) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "rps_set_config first");
-  if (ctx->mode == RPS_MODE_NBODY && ctx->nranks > 1 && !ctx->comm)
+  const bool nb_external = (ctx->ext.flags & RPS_EXT_NBODY_EXTERNAL) != 0;
+  if (ctx->mode == RPS_MODE_NBODY && ctx->nranks > 1 && !ctx->comm && !nb_external)
     return fail(ctx, RPS_ERR_COMM, "sharded N-body needs rps_comm_init");
-  if (ctx->mode == RPS_MODE_NBODY && ctx->global_count != ctx->n && !ctx->comm)
-    return fail(ctx, RPS_ERR_COMM, "sharded N-body needs rps_comm_init");
+  if (ctx->mode == RPS_MODE_NBODY && ctx->global_count != ctx->n && !ctx->comm && !nb_external)
+    return fail(ctx, RPS_ERR_COMM, "sharded N-body needs rps_comm_init or RPS_EXT_NBODY_EXTERNAL");
   const uint32_t fuse = std::min<uint32_t>(ctx->ext.fuse_steps, kMaxFuse);
   const bool fused = ctx->mode == RPS_MODE_STREAM && fuse > 1;
   const uint32_t interval = std::max<uint32_t>(ctx->ext.stats_interval, 1u);
@@ -970,6 +976,19 @@ int rps_step_cost(const rps_ctx* ctx, double* amount, int* unit) {
     default:
       return fail(const_cast<rps_ctx*>(ctx), RPS_ERR_UNSUPPORTED, "no closed-form cost for SPH mode");
   }
+}
+
+int rps_nbody_sources(rps_ctx* ctx, int pack, void** sources, uint64_t* count) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (ctx->mode != RPS_MODE_NBODY) return fail(ctx, RPS_ERR_UNSUPPORTED, "N-body mode only");
+  if (pack) {
+    RPS_HIP(ctx, launch_nbody_pack(ctx->x, ctx->y, ctx->pos_all + ctx->id_offset, ctx->n, ctx->stream));
+    RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  }
+  if (sources) *sources = ctx->pos_all;
+  if (count) *count = ctx->global_count;
+  return RPS_OK;
 }
 
 int rps_comm_unique_id(void* out128) {

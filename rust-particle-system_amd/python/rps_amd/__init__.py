@@ -42,7 +42,7 @@ RPS_ERR_NO_DEVICE = 6
 
 MODE_STREAM, MODE_NBODY, MODE_SPH = 0, 1, 2
 EULER, VERLET = 0, 1
-EXT_LIFETIME, EXT_STATS = 1, 2
+EXT_LIFETIME, EXT_STATS, EXT_NBODY_EXTERNAL = 1, 2, 4
 MAX_ATTRACTORS = 8
 FIELD_X, FIELD_Y, FIELD_VX, FIELD_VY, FIELD_LIFE = 0, 1, 2, 3, 4
 FIELD_LIFE_STEPS = 5  # whole lifetime steps left (exact); FIELD_LIFE = that * dt seconds
@@ -180,6 +180,7 @@ ABI_SYMBOLS = [
     ("rps_get_stream", _P, [_P]),
     ("rps_step_cost", _I, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I)]),
     ("rps_comm_unique_id", _I, [_P]),
+    ("rps_nbody_sources", _I, [_P, _I, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(_U64)]),
     ("rps_comm_init", _I, [_P, _I, _I, _P]),
 ]
 
@@ -509,6 +510,12 @@ class Context:
         amt, unit = ctypes.c_double(), ctypes.c_int()
         self._call("rps_step_cost", ctypes.byref(amt), ctypes.byref(unit))
         return amt.value, ("bytes" if unit.value == 0 else "flops")
+
+    def nbody_sources(self, pack: bool = True):
+        """(device pointer, count) of the global float2 source array (rps_nbody_sources)."""
+        ptr, cnt = ctypes.c_void_p(), ctypes.c_uint64()
+        self._call("rps_nbody_sources", 1 if pack else 0, ctypes.byref(ptr), ctypes.byref(cnt))
+        return ptr.value, cnt.value
 
     def comm_init(self, rank: int, nranks: int, unique_id: bytes):
         buf = ctypes.create_string_buffer(bytes(unique_id), 128)

@@ -21,6 +21,11 @@ def hip():
     return _hip
 
 
+def copy_d2d(dst, src, nbytes):
+    """hipMemcpy device -> device (raw pointers as ints)."""
+    assert hip().hipMemcpy(ctypes.c_void_p(dst), ctypes.c_void_p(src), nbytes, 3) == 0
+
+
 class DeviceBuffer:
     def __init__(self, nbytes):
         self.ptr = ctypes.c_void_p()

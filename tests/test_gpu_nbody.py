@@ -94,3 +94,47 @@ def test_nbody_single_rank_comm(gpu, orc):
         ay = ctx.read_debug(rps.DEBUG_ACCEL_Y)
     rx, ry = orc.nbody_accel(ext, soa["x"], soa["y"])
     _check_accel(ax, ay, rx, ry, ext, soa["x"], soa["y"])
+
+
+def test_nbody_sharded_external_exchange(gpu, orc):
+    """The sharded all-pairs data path on one GPU: 4 shard contexts (id_offset r*n, global
+    4n) whose sources are exchanged by the caller (RPS_EXT_NBODY_EXTERNAL + rps_nbody_sources,
+    device-to-device copies standing in for the ncclAllGather of multi-GPU runs).  Each
+    shard's accelerations match the unsharded oracle for its targets; the integration given
+    them is bitwise; two steps keep the shards consistent."""
+    from hip_mem import copy_d2d
+
+    rps = gpu
+    R, n = 4, 2048
+    N = R * n
+    cfg = config_c1(rps, N)
+    ext = rps.make_ext(nbody_strength=20.0, nbody_softening=1.5, drag=0.05, shader_delay=0)
+    ext.flags |= rps.EXT_NBODY_EXTERNAL
+    g = np.random.default_rng(77)
+    full = dict(x=g.uniform(-900, 900, N).astype(F), y=g.uniform(-500, 500, N).astype(F),
+                vx=g.normal(0, 10, N).astype(F), vy=g.normal(0, 10, N).astype(F))
+    ctxs = [rps.Context(n, rps.MODE_NBODY, id_offset=r * n, global_count=N) for r in range(R)]
+    try:
+        for r, c in enumerate(ctxs):
+            c.set_config(cfg, ext)
+            c.upload_soa({k: v[r * n:(r + 1) * n] for k, v in full.items()})
+        ref = copy_soa(full)
+        for step in range(2):
+            srcs = [c.nbody_sources(pack=True) for c in ctxs]
+            assert all(cnt == N for _, cnt in srcs)
+            for r in range(R):
+                for q in range(R):
+                    if q != r:
+                        copy_d2d(srcs[r][0] + q * n * 8, srcs[q][0] + q * n * 8, n * 8)
+            for c in ctxs:
+                c.step(1)
+            rx, ry = orc.nbody_accel(ext, ref["x"], ref["y"])
+            got_ax = np.concatenate([c.read_debug(rps.DEBUG_ACCEL_X) for c in ctxs])
+            got_ay = np.concatenate([c.read_debug(rps.DEBUG_ACCEL_Y) for c in ctxs])
+            _check_accel(got_ax, got_ay, rx, ry, ext, ref["x"], ref["y"])
+            orc.nbody_integrate(cfg, ext, got_ax, got_ay, ref)  # bitwise given the device accel
+            got = {k: np.concatenate([c.download_soa()[k] for c in ctxs]) for k in ("x", "y", "vx", "vy")}
+            assert_soa_bitwise(got, ref, what=f"step{step} ")
+    finally:
+        for c in ctxs:
+            c.close()
