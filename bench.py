@@ -3,8 +3,8 @@
 
 Workload (BASELINE.json configs[2]): 1e8 particles per GPU, 4 attractors
 moving on circles, drag, lifetime decay + Philox respawn, semi-implicit Euler, walls.  One
-"step" = one fused stream-kernel launch over every particle (in place, SoA, 40 B/particle
-of algorithmic HBM traffic).  Multi-GPU: one process per GPU, contiguous index shards with
+"step" = one fused stream-kernel launch over every particle (in place, tiled SoA, 34 B/particle
+of algorithmic HBM traffic: x, y, vx, vy read+written, the u16 lifetime expiry read).  Multi-GPU: one process per GPU, contiguous index shards with
 global particle ids, no data-path collective (weak scaling: 1e8 particles per rank).
 
     python bench.py [--gpus N --steps K --warmup W]

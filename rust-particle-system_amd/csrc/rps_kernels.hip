@@ -822,7 +822,7 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
 }
 
 // simulation_step, compute_shader.wgsl:435-453: pressure (:256-334) and viscosity
-// (:336-384) against the start-of-pass velocity snapshot (vel_s), Euler (:392-395) and walls
+// (:336-384) against the start-of-pass velocity snapshot (dv_s.zw), Euler (:392-395) and walls
 // (:69-99).  New velocities/positions go to (vx2, vy2, x2, y2).
 template <int kScanBatch>
 __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __restrict__ cfg,
