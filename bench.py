@@ -3,9 +3,11 @@
 
 Workload (BASELINE.json configs[2]): 1e8 particles per GPU, 4 attractors
 moving on circles, drag, lifetime decay + Philox respawn, semi-implicit Euler, walls.  One
-"step" = one fused stream-kernel launch over every particle (in place, tiled SoA, 34 B/particle
-of algorithmic HBM traffic: x, y, vx, vy read+written, the u16 lifetime expiry read).  Multi-GPU: one process per GPU, contiguous index shards with
-global particle ids, no data-path collective (weak scaling: 1e8 particles per rank).
+"step" = one fused stream-kernel launch over every particle (in place, tiled SoA, 34 B per
+particle of algorithmic HBM traffic: x, y, vx, vy read+written, the u16 lifetime expiry
+read).  Multi-GPU: one process per GPU, contiguous index shards with global particle ids, no
+data-path collective (weak scaling: 1e8 particles per rank).  Side line "allpairs": the
+all-pairs N-body step with its RCCL all-gather, strong-scaled over the ranks.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
