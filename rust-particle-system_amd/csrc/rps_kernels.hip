@@ -1209,7 +1209,7 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
   }
   // Tile: 2048 entries up to P = 2^18 (enough workgroups to fill the chip in the LDS
   // passes), 8192 above (fewer global passes; measured at 50 k / 1 M / 4 M particles).
-  const uint32_t want = P <= (1u << 18) ? 2048u : kSortTile;
+  const uint32_t want = P <= (1u << 18) ? 2048u : kSortTile;  // 1024/4096/8192 measured slower
   const uint32_t tile = P < want ? P : want;
   uint32_t tile_log = 0;
   while ((1u << tile_log) < tile) ++tile_log;

@@ -119,6 +119,10 @@ if __name__ == "__main__":
         cpu_sph(1 << 20, frames=3)
         cpu_nbody()
         sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "sph_small":
+        for n in (16384, 65536, 1 << 18):
+            sph(n)
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "sph":
         for n in (50000, 65536, 1 << 20, 1 << 22):
             sph(n)
