@@ -40,10 +40,11 @@ struct rps_ctx {
   float* state = nullptr;          // STREAM: the tiled x|y|vx|vy|expiry block
   float *x = nullptr, *y = nullptr, *vx = nullptr, *vy = nullptr;
   uint16_t* exp = nullptr;         // STREAM: lifetime expiry (u16)
-  // SPH
-  float *vx2 = nullptr, *vy2 = nullptr, *x2 = nullptr, *y2 = nullptr;
-  uint4* rec_s = nullptr;  // SPH slot records (rps_internal.hpp SphBuffers)
-  f4* dv_s = nullptr;
+  // SPH: packed {x, y, vx, vy} state (x..vy point into st, layout sph_layout())
+  f4* st = nullptr;
+  f4* st2 = nullptr;       // sim-pass output, swapped with st after the pass
+  SphSlots sl{};           // SPH slot records (rps_internal.hpp)
+  uint32_t* ends = nullptr;
   uint2* lookup = nullptr;
   uint32_t* offsets = nullptr;
   f2* dens = nullptr;
@@ -247,19 +248,24 @@ int prof_end(rps_ctx* ctx) {
   return RPS_OK;
 }
 
+// SPH state: packed float4 per particle, so the field views are a layout (offset 4i).
+Layout sph_layout() { return Layout{0, 4, 0}; }
+
+void set_sph_fields(rps_ctx* ctx) {
+  float* base = reinterpret_cast<float*>(ctx->st);
+  ctx->x = base;
+  ctx->y = base + 1;
+  ctx->vx = base + 2;
+  ctx->vy = base + 3;
+}
+
 SphBuffers sph_buffers(rps_ctx* ctx) {
   SphBuffers b;
   b.cfg = ctx->d_cfg;
-  b.x = ctx->x;
-  b.y = ctx->y;
-  b.vx = ctx->vx;
-  b.vy = ctx->vy;
-  b.vx2 = ctx->vx2;
-  b.vy2 = ctx->vy2;
-  b.x2 = ctx->x2;
-  b.y2 = ctx->y2;
-  b.rec_s = ctx->rec_s;
-  b.dv_s = ctx->dv_s;
+  b.st = ctx->st;
+  b.st2 = ctx->st2;
+  b.sl = ctx->sl;
+  b.ends = ctx->ends;
   b.lookup = ctx->lookup;
   b.offsets = ctx->offsets;
   b.dens = ctx->dens;
@@ -403,10 +409,8 @@ int step_sph_sim(rps_ctx* ctx) {
   RPS_HIP(ctx, launch_sph_sim(b, ctx->stream));
   rc = prof_end(ctx);
   if (rc) return rc;
-  std::swap(ctx->vx, ctx->vx2);
-  std::swap(ctx->vy, ctx->vy2);
-  std::swap(ctx->x, ctx->x2);
-  std::swap(ctx->y, ctx->y2);
+  std::swap(ctx->st, ctx->st2);
+  set_sph_fields(ctx);
   return RPS_OK;
 }
 
@@ -500,7 +504,7 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     // Tiled SoA: ceil(n / kTile) tiles of 4 f32 + 1 u16 segments (rps_device.hpp).
     const size_t tiles = (n + kTile - 1) / kTile;
     slots.push_back({(void**)&ctx->state, tiles * kTileBytes});
-  } else {
+  } else if (ctx->mode == RPS_MODE_NBODY) {
     slots.push_back({(void**)&ctx->x, nf});
     slots.push_back({(void**)&ctx->y, nf});
     slots.push_back({(void**)&ctx->vx, nf});
@@ -508,12 +512,16 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
   }
   if (ctx->mode == RPS_MODE_SPH) {
     ctx->P = next_pow2_u32((uint32_t)n);  // spatial lookup sized next_pow2 (particle_buffers.rs:86)
-    slots.push_back({(void**)&ctx->vx2, nf});
-    slots.push_back({(void**)&ctx->vy2, nf});
-    slots.push_back({(void**)&ctx->x2, nf});
-    slots.push_back({(void**)&ctx->y2, nf});
-    slots.push_back({(void**)&ctx->rec_s, align_up((size_t)ctx->P * sizeof(uint4), 256)});
-    slots.push_back({(void**)&ctx->dv_s, align_up((size_t)ctx->P * sizeof(f4), 256)});
+    const size_t P = ctx->P;
+    slots.push_back({(void**)&ctx->st, align_up(n * sizeof(f4), 256)});
+    slots.push_back({(void**)&ctx->st2, align_up(n * sizeof(f4), 256)});
+    slots.push_back({(void**)&ctx->sl.pp_s, align_up(P * sizeof(f2), 256)});
+    slots.push_back({(void**)&ctx->sl.rec_pv, align_up(P * sizeof(f4), 256)});
+    slots.push_back({(void**)&ctx->sl.rec_pd, align_up(P * sizeof(f4), 256)});
+    slots.push_back({(void**)&ctx->sl.dens_s, align_up(P * sizeof(f2), 256)});
+    slots.push_back({(void**)&ctx->sl.idx_s, align_up(P * sizeof(uint32_t), 256)});
+    slots.push_back({(void**)&ctx->sl.cur_s, align_up(P * sizeof(f2), 256)});
+    slots.push_back({(void**)&ctx->ends, align_up(n * sizeof(uint32_t), 256)});
     slots.push_back({(void**)&ctx->lookup, align_up((size_t)ctx->P * sizeof(uint2), 256)});
     slots.push_back({(void**)&ctx->offsets, align_up(n * sizeof(uint32_t), 256)});
     slots.push_back({(void**)&ctx->dens, align_up(n * sizeof(f2), 256)});
@@ -542,6 +550,10 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     return bail(e == hipErrorOutOfMemory ? RPS_ERR_OUT_OF_MEMORY : RPS_ERR_DEVICE);
   }
   for (size_t i = 0; i < slots.size(); ++i) *slots[i].p = ctx->arena + offs[i];
+  if (ctx->mode == RPS_MODE_SPH) {
+    ctx->layout = sph_layout();
+    set_sph_fields(ctx);
+  }
   if (ctx->mode == RPS_MODE_STREAM) {
     ctx->layout = tiled_layout();
     ctx->x = ctx->state;
@@ -769,7 +781,7 @@ int rps_read_debug(rps_ctx* ctx, int which, void* dst, uint64_t bytes) {
   switch (which) {
     case RPS_DEBUG_SPATIAL_LOOKUP: src = ctx->lookup; want = (uint64_t)ctx->P * 8; break;
     case RPS_DEBUG_LOOKUP_OFFSETS: src = ctx->offsets; want = ctx->n * 4; break;
-    case RPS_DEBUG_DENSITIES: src = ctx->dens; want = ctx->n * 8; break;
+    case RPS_DEBUG_DENSITIES: src = ctx->dens; want = ctx->n * 8; break;  // rebuilt below
     case RPS_DEBUG_PREDICTED: src = ctx->pred; want = ctx->n * 8; break;
     case RPS_DEBUG_ACCEL_X: src = ctx->ax; want = ctx->n * 4; break;
     case RPS_DEBUG_ACCEL_Y: src = ctx->ay; want = ctx->n * 4; break;
@@ -794,6 +806,8 @@ int rps_read_debug(rps_ctx* ctx, int which, void* dst, uint64_t bytes) {
     }
     return RPS_OK;
   }
+  if (which == RPS_DEBUG_DENSITIES || which == RPS_DEBUG_PREDICTED)
+    RPS_HIP(ctx, launch_sph_debug_views(sph_buffers(ctx), ctx->stream));
   RPS_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
   RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return RPS_OK;

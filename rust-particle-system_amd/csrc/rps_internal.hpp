@@ -82,25 +82,26 @@ struct NbodyIntegrateArgs {
 hipError_t launch_nbody_integrate(const NbodyIntegrateArgs& a, hipStream_t s);
 
 // SPH (the reference's five passes).
+// Per-slot records in spatial-lookup order (slot t holds particle lookup[t].y's values), so
+// a run's entries are contiguous.  Written by the predict pass except rec_pd (density pass).
+struct SphSlots {
+  f2* pp_s;      // P predicted positions                    (density scan: 8 B/entry)
+  f4* rec_pv;    // P {predicted x, y, post-gravity vx, vy}  (viscosity scan)
+  f4* rec_pd;    // P {predicted x, y, P/rho^2, Pn/(rho rho_n)} (pressure scan)
+  f2* dens_s;    // P {density, near density}
+  uint32_t* idx_s;  // P particle index (self-skip, wgsl:295 / :365)
+  f2* cur_s;     // P current positions (Euler base)
+};
 struct SphBuffers {
   const rps_config* cfg;  // device-resident ParticleConfig
-  float* x;
-  float* y;
-  float* vx;    // current velocities (snapshot for neighbours in the sim pass)
-  float* vy;
-  float* vx2;   // sim-pass output velocities (swapped with vx/vy after the pass)
-  float* vy2;
-  float* x2;    // sim-pass output positions (swapped with x/y after the pass)
-  float* y2;
+  const f4* st;      // N packed {x, y, vx, vy}: the state at the start of the frame
+  f4* st2;           // N: sim-pass output (swapped with st after the pass)
   uint2* lookup;     // P entries
-  uint32_t* offsets; // N
-  f2* dens;          // N
+  uint32_t* offsets; // N: first slot of each key's run (wgsl:55)
+  uint32_t* ends;    // N: one past the last slot of each key's run in [0, N)
+  f2* dens;          // N  debug views (wgsl:58, :61), rebuilt on readback
   f2* pred;          // N
-  // Neighbour data in spatial-lookup order (slot j holds particle lookup[j].y's values), so
-  // a cell's entries are contiguous: rec_s and dv_s.zw after prediction, dv_s.xy after the
-  // density pass.
-  uint4* rec_s;      // P slot records {key, index, predicted x, y}
-  f4* dv_s;          // P {density, near density, post-gravity vx, vy}
+  SphSlots sl;
   uint32_t n;        // N
   uint32_t p;        // next_pow2(N)
 };
@@ -111,5 +112,7 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
 hipError_t launch_sph_offsets(const SphBuffers& b, hipStream_t s);
 hipError_t launch_sph_pre(const SphBuffers& b, hipStream_t s);
 hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s);
+// Rebuild the per-particle predicted-position and density buffers from the slot records.
+hipError_t launch_sph_debug_views(const SphBuffers& b, hipStream_t s);
 
 }  // namespace rps

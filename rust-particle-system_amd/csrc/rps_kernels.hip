@@ -635,16 +635,16 @@ constexpr uint32_t kSortFuse = 4;     // global passes per register-fused launch
 // what the previous frame's sort left there (the reference never rewrites them).
 struct SortBin {
   const rps_config* cfg;
-  const float* x;
-  const float* y;
+  const f4* st;  // packed {x, y, vx, vy} per particle
   uint32_t* offsets;
   uint32_t n;
 };
 
 __device__ __forceinline__ uint2 bin_entry(const SortBin& b, uint32_t i) {
   const float r = b.cfg->smoothing_radius;
-  const int32_t cx = f32_to_i32((b.x[i] + b.cfg->screen_bounds[1]) / r);
-  const int32_t cy = f32_to_i32((b.y[i] + b.cfg->screen_bounds[3]) / r);
+  const f2 pos = reinterpret_cast<const f2*>(b.st)[2u * i];
+  const int32_t cx = f32_to_i32((pos[0] + b.cfg->screen_bounds[1]) / r);
+  const int32_t cy = f32_to_i32((pos[1] + b.cfg->screen_bounds[3]) / r);
   b.offsets[i] = 0xFFFFFFFFu;
   return make_uint2(cell_key(cx, cy, b.cfg->particle_count), i);
 }
@@ -696,269 +696,277 @@ __global__ __launch_bounds__(1024) void sph_sort_local_kernel(
   for (uint32_t q = threadIdx.x; q < tile; q += blockDim.x) lookup[base0 + q] = s[q];
 }
 
-// calculate_spatial_lookup_offsets, compute_shader.wgsl:507-525.
+// calculate_spatial_lookup_offsets, compute_shader.wgsl:507-525: offsets[key] = the first
+// slot of key's run.  The same pass also records ends[key] = one past the run's last slot
+// in [0, n): the reference's scan of a run stops at the first slot whose key differs or at
+// N (wgsl:233-237), and the sorted prefix [0, N) holds each key's entries contiguously, so
+// [offsets[key], ends[key]) is exactly the set of slots it visits, in the same order.
+// (ends[] needs no reset: it is read only for keys whose offsets entry this frame set.)
 __global__ __launch_bounds__(kBlock) void sph_offsets_kernel(const uint2* __restrict__ lookup,
                                                              uint32_t* __restrict__ offsets,
+                                                             uint32_t* __restrict__ ends,
                                                              uint32_t n) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   const uint32_t key = lookup[i].x;
   const uint32_t prev = i > 0u ? lookup[i - 1u].x : 0xFFFFFFFFu;
+  const uint32_t next = i + 1u < n ? lookup[i + 1u].x : 0xFFFFFFFFu;
   if (key != prev) offsets[key] = i;
+  if (key != next || i + 1u == n) ends[key] = i + 1u;
 }
 
 __constant__ int32_t kGridOff[9][2] = {{-1, -1}, {-1, 0}, {-1, 1}, {0, -1}, {0, 0},
                                        {0, 1},   {1, -1}, {1, 0},  {1, 1}};
 
 // pre_simulation_step part 1 (wgsl:397-405) in lookup order: slot t (of all P) takes
-// particle i = lookup[t].y, applies gravity and predicts, and writes the results to slot t
-// and pred[i]: the slot record rec_s[t] = {key, i, predicted x, y} and dv_s[t].zw = the
-// post-gravity velocity (dv_s[t].xy gets the densities in the density pass).  The density
-// and sim passes then read a complete snapshot, a cell's entries
-// contiguously with one 16-B load per record, and their own particle at their own slot.
-// Pad slots repeat some particle and write identical values.
+// particle i = lookup[t].y (one 16-B gather of its packed state), applies gravity and
+// predicts, and writes slot-ordered records that the later passes read contiguously
+// (SphBuffers: pp_s, rec_pv, idx_s, cur_s).  The density and sim passes therefore read a
+// complete snapshot.  The reference's per-particle predicted_positions /
+// densities buffers are not written on the hot path; launch_sph_debug_views rebuilds them
+// from the slot records on readback.  Pad slots repeat some particle and
+// write identical values.
 __global__ __launch_bounds__(kBlock) void sph_predict_kernel(const rps_config* __restrict__ cfg,
                                                              const uint2* __restrict__ lookup,
-                                                             const float* __restrict__ x,
-                                                             const float* __restrict__ y,
-                                                             const float* __restrict__ vx,
-                                                             const float* __restrict__ vy,
-                                                             f2* __restrict__ pred,
-                                                             uint4* __restrict__ rec_s,
-                                                             f4* __restrict__ dv_s,
-                                                             uint32_t p_slots) {
+                                                             const f4* __restrict__ st,
+                                                             SphSlots sl, uint32_t p_slots) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= p_slots) return;
-  const uint2 e = lookup[t];
-  const uint32_t i = e.y;
+  const uint32_t i = lookup[t].y;
+  const f4 s = st[i];
   const float dt = cfg->fixed_delta_time;
-  const float qx = vx[i] + 0.0f * dt;  // apply_gravity, wgsl:397-400
-  const float qy = vy[i] + (-cfg->gravity) * dt;
-  const f2 p = f2{x[i] + qx * dt, y[i] + qy * dt};  // wgsl:402-405
-  rec_s[t] = make_uint4(e.x, i, __float_as_uint(p[0]), __float_as_uint(p[1]));
-  reinterpret_cast<f2*>(dv_s)[2 * t + 1] = f2{qx, qy};
-  pred[i] = p;
+  const float qx = s[2] + 0.0f * dt;  // apply_gravity, wgsl:397-400
+  const float qy = s[3] + (-cfg->gravity) * dt;
+  const float px = s[0] + qx * dt, py = s[1] + qy * dt;  // wgsl:402-405
+  sl.pp_s[t] = f2{px, py};
+  sl.rec_pv[t] = f4{px, py, qx, qy};
+  sl.idx_s[t] = i;
+  sl.cur_s[t] = f2{s[0], s[1]};
 }
 
-// kScanBatch: lookup entries in flight per lane in the neighbour scans (template).
+// The nine runs a particle at predicted position p scans, in the reference's cell order
+// (wgsl:223-224 / :277-278), flattened: entry f (0 <= f < total) of the concatenation is
+// slot f + adj[o] for the cell o with cum[o] <= f < cum[o+1].  The 18 offsets/ends loads
+// are issued together.  A key absent from [0, N) has offsets 0xFFFFFFFF: an empty run.
+struct NineRuns {
+  uint32_t cum[9];  // entries before cell o
+  uint32_t adj[9];  // slot - flat index inside cell o (mod 2^32)
+  uint32_t total;
+};
 
 __device__ __forceinline__ uint32_t grid_key(int32_t cx, int32_t cy, int o, uint32_t N) {
   return cell_key((int32_t)((uint32_t)cx + (uint32_t)kGridOff[o][0]),
                   (int32_t)((uint32_t)cy + (uint32_t)kGridOff[o][1]), N);
 }
 
-// The 3x3 cells around (cx, cy) in the reference's order (wgsl:223-224 / :277-278): their
-// keys and first lookup slots, the nine offsets loads issued together.
-__device__ __forceinline__ void cell_starts(const uint32_t* __restrict__ offsets, int32_t cx,
-                                            int32_t cy, uint32_t N, uint32_t keys[9],
-                                            uint32_t starts[9]) {
+__device__ __forceinline__ NineRuns nine_runs(const uint32_t* __restrict__ offsets,
+                                              const uint32_t* __restrict__ ends, float px, float py,
+                                              float xoff, float yoff, float r, uint32_t N) {
+  const int32_t cx = f32_to_i32((px + xoff) / r);  // particle_position_to_cell_coord, wgsl:121-130
+  const int32_t cy = f32_to_i32((py + yoff) / r);
+  uint32_t key[9], s[9], e[9];
 #pragma unroll
-  for (int o = 0; o < 9; ++o) keys[o] = grid_key(cx, cy, o, N);
+  for (int o = 0; o < 9; ++o) key[o] = grid_key(cx, cy, o, N);
 #pragma unroll
-  for (int o = 0; o < 9; ++o) starts[o] = offsets[keys[o]];
+  for (int o = 0; o < 9; ++o) {
+    s[o] = offsets[key[o]];
+    e[o] = ends[key[o]];
+  }
+  NineRuns R;
+  uint32_t c = 0;
+#pragma unroll
+  for (int o = 0; o < 9; ++o) {
+    const uint32_t len = s[o] < N ? e[o] - s[o] : 0u;
+    R.cum[o] = c;
+    R.adj[o] = s[o] - c;
+    c += len;
+  }
+  R.total = c;
+  return R;
 }
 
-// Work mapping of the density and sim passes: thread t takes the particle in lookup slot t,
-// t in [0, P).  Lanes of a wave then hold spatially adjacent particles and scan the same
-// cells.  Every particle's fresh entry is in exactly one slot; pad slots
-// repeat some particle, whose recomputation writes the identical value (all outputs are
-// separate buffers), so the race is benign and results are independent of it.
+// Slot of flat entry f (f < total): the last cell whose run starts at or before f.  Cells
+// with empty runs share their successor's cum and are skipped by the >= chain.
+__device__ __forceinline__ uint32_t run_slot(const NineRuns& R, uint32_t f) {
+  uint32_t j = f + R.adj[0];
+#pragma unroll
+  for (int o = 1; o < 9; ++o) j = f >= R.cum[o] ? f + R.adj[o] : j;
+  return j;
+}
+
+// Work mapping of the density and sim passes: thread t takes lookup slot t of all P.  Lanes
+// of a wave then hold the particles of a few cells and read the same runs together.  Every
+// particle's fresh entry is in exactly one slot; pad slots repeat some
+// particle, whose recomputation writes the identical value (outputs are separate buffers),
+// so the race is benign and results are independent of it.
 //
-// calculate_density, compute_shader.wgsl:207-254, entries summed in lookup order.
+// calculate_density, compute_shader.wgsl:207-254: entries summed in run order, kScanBatch
+// predicted positions in flight per lane across run boundaries.
 template <int kScanBatch>
 __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* __restrict__ cfg,
                                                              const uint32_t* __restrict__ offsets,
-                                                             const uint4* __restrict__ rec_s,
-                                                             f2* __restrict__ dens,
-                                                             f4* __restrict__ dv_s,
-                                                             uint32_t p_slots) {
+                                                             const uint32_t* __restrict__ ends,
+                                                             SphSlots sl, uint32_t p_slots) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= p_slots) return;
-  const uint4 own = rec_s[t];
-  const uint32_t i = own.y;
+  const f2 p = sl.pp_s[t];
   const float r = cfg->smoothing_radius, r2 = r * r;
   const uint32_t N = cfg->particle_count;
   const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
-  const f2 p = f2{__uint_as_float(own.z), __uint_as_float(own.w)};
-  const int32_t cx = f32_to_i32((p[0] + cfg->screen_bounds[1]) / r);
-  const int32_t cy = f32_to_i32((p[1] + cfg->screen_bounds[3]) / r);
-  uint32_t keys[9], starts[9];
-  cell_starts(offsets, cx, cy, N, keys, starts);
+  const NineRuns R = nine_runs(offsets, ends, p[0], p[1], cfg->screen_bounds[1],
+                               cfg->screen_bounds[3], r, N);
   float d = 0.0f, nd = 0.0f;
-  for (int o = 0; o < 9; ++o) {
-    const uint32_t key = keys[o];
-    for (uint32_t j = starts[o]; j < N; j += kScanBatch) {
-      uint4 e[kScanBatch];
+  for (uint32_t f = 0; f < R.total; f += kScanBatch) {
+    f2 q[kScanBatch];
 #pragma unroll
-      for (int u = 0; u < kScanBatch; ++u) e[u] = rec_s[min(j + u, N - 1u)];
-      bool stop = false;
+    for (int u = 0; u < kScanBatch; ++u)
+      q[u] = sl.pp_s[run_slot(R, min(f + u, R.total - 1u))];
 #pragma unroll
-      for (int u = 0; u < kScanBatch; ++u) {
-        if (!stop) {
-          if (j + u >= N || e[u].x != key) {
-            stop = true;
-          } else {
-            const float dx = p[0] - __uint_as_float(e[u].z), dy = p[1] - __uint_as_float(e[u].w);
-            const float sq = dx * dx + dy * dy;
-            if (!(sq > r2)) {
-              const float dist = sqrtf(sq);
-              float k1 = 0.0f, k2 = 0.0f;
-              if (!(dist >= r)) {
-                const float v = r - dist;
-                k1 = (dn * v) * v;
-                k2 = ((ndn * v) * v) * v;
-              }
-              d = d + k1;
-              nd = nd + k2;
-            }
+    for (int u = 0; u < kScanBatch; ++u) {
+      if (f + u < R.total) {
+        const float dx = p[0] - q[u][0], dy = p[1] - q[u][1];
+        const float sq = dx * dx + dy * dy;
+        if (!(sq > r2)) {
+          const float dist = sqrtf(sq);
+          float k1 = 0.0f, k2 = 0.0f;
+          if (!(dist >= r)) {
+            const float v = r - dist;
+            k1 = (dn * v) * v;
+            k2 = ((ndn * v) * v) * v;
           }
+          d = d + k1;
+          nd = nd + k2;
         }
       }
-      if (stop) break;
     }
   }
-  dens[i] = f2{d, nd};
-  reinterpret_cast<f2*>(dv_s)[2 * t] = f2{d, nd};
+  // The neighbour halves of pressure_term / near_pressure_term (wgsl:323-327) depend on this
+  // particle alone: evaluated once here (same ops, same bits) instead of per visiting
+  // neighbour in the sim pass.
+  const float P = (d - cfg->target_density) * cfg->pressure_multiplier;  // wgsl:191-199
+  const float Pn = nd * cfg->near_density_multiplier;
+  sl.rec_pd[t] = f4{p[0], p[1], P / (d * d), Pn / (d * nd)};
+  sl.dens_s[t] = f2{d, nd};
 }
 
 // simulation_step, compute_shader.wgsl:435-453: pressure (:256-334) and viscosity
-// (:336-384) against the start-of-pass velocity snapshot (dv_s.zw), Euler (:392-395) and walls
-// (:69-99).  New velocities/positions go to (vx2, vy2, x2, y2).
+// (:336-384) against the start-of-pass velocity snapshot (rec_pv.zw), Euler (:392-395) and
+// walls (:69-99).  The new packed state of particle i goes to st2[i].
 template <int kScanBatch>
 __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __restrict__ cfg,
                                                          const uint32_t* __restrict__ offsets,
-                                                         const uint4* __restrict__ rec_s,
-                                                         const f4* __restrict__ dv_s,
-                                                         const float* __restrict__ x,
-                                                         const float* __restrict__ y,
-                                                         float* __restrict__ vx2,
-                                                         float* __restrict__ vy2,
-                                                         float* __restrict__ x2,
-                                                         float* __restrict__ y2, uint32_t p_slots) {
+                                                         const uint32_t* __restrict__ ends,
+                                                         SphSlots sl, f4* __restrict__ st2,
+                                                         uint32_t p_slots) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= p_slots) return;
-  const uint4 own = rec_s[t];
-  const f4 own_dv = dv_s[t];  // own densities (xy) and post-gravity velocity (zw)
-  const uint32_t i = own.y;
+  const f4 own = sl.rec_pd[t];  // own predicted position (xy) and P / rho^2 (z)
+  const f2 own_d = sl.dens_s[t];
+  const uint32_t i = sl.idx_s[t];
   const float dt = cfg->fixed_delta_time;
   const float r = cfg->smoothing_radius, r2 = r * r;
   const uint32_t N = cfg->particle_count;
-  const float td = cfg->target_density, pm = cfg->pressure_multiplier;
-  const float nm = cfg->near_density_multiplier;
   const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
   const float vn = cfg->viscocity_kernel_norm;
-  const f2 p = f2{__uint_as_float(own.z), __uint_as_float(own.w)};
-  const int32_t cx = f32_to_i32((p[0] + cfg->screen_bounds[1]) / r);
-  const int32_t cy = f32_to_i32((p[1] + cfg->screen_bounds[3]) / r);
-  const float rho = own_dv[0], rhon = own_dv[1];
-  const float P = (rho - td) * pm;
-  const float Pn = rhon * nm;
-  const float P_rho2 = P / (rho * rho);    // loop-invariant halves of pressure_term and
+  const f2 p = f2{own[0], own[1]};
+  const float rho = own_d[0];
+  const float Pn = own_d[1] * cfg->near_density_multiplier;
+  const float P_rho2 = own[2];             // loop-invariant halves of pressure_term and
   const float Pn_rho2 = Pn / (rho * rho);  // near_pressure_term (wgsl:323-327)
-  uint32_t keys[9], starts[9];
-  cell_starts(offsets, cx, cy, N, keys, starts);
+  const NineRuns R = nine_runs(offsets, ends, p[0], p[1], cfg->screen_bounds[1],
+                               cfg->screen_bounds[3], r, N);
   float fx = 0.0f, fy = 0.0f;
-  for (int o = 0; o < 9; ++o) {
-    const uint32_t key = keys[o];
-    for (uint32_t j = starts[o]; j < N; j += kScanBatch) {
-      uint4 e[kScanBatch];
-      f2 dj[kScanBatch];
+  for (uint32_t f = 0; f < R.total; f += kScanBatch) {
+    f4 q[kScanBatch];
+    uint32_t qi[kScanBatch];
 #pragma unroll
-      for (int u = 0; u < kScanBatch; ++u) {
-        const uint32_t jj = min(j + u, N - 1u);
-        e[u] = rec_s[jj];
-        dj[u] = reinterpret_cast<const f2*>(dv_s)[2 * jj];
-      }
-      bool stop = false;
+    for (int u = 0; u < kScanBatch; ++u) {
+      const uint32_t j = run_slot(R, min(f + u, R.total - 1u));
+      q[u] = sl.rec_pd[j];
+      qi[u] = sl.idx_s[j];
+    }
 #pragma unroll
-      for (int u = 0; u < kScanBatch; ++u) {
-        if (!stop) {
-          if (j + u >= N || e[u].x != key) {
-            stop = true;
-          } else if (e[u].y != i) {
-            const float dx = __uint_as_float(e[u].z) - p[0], dy = __uint_as_float(e[u].w) - p[1];
-            const float sq = dx * dx + dy * dy;
-            if (!(sq > r2)) {
-              const float dist = sqrtf(sq);
-              float dirx, diry;
-              if (dist > 0.0001f) {
-                dirx = dx / dist;
-                diry = dy / dist;
-              } else {
-                dirx = 0.0f;
-                diry = 1.0f;
-              }
-              const float rj = dj[u][0], rnj = dj[u][1];
-              const float Pj = (rj - td) * pm;
-              const float Pnj = rnj * nm;
-              const float pt = P_rho2 + (Pj / (rj * rj));
-              const float npt = Pn_rho2 + (Pnj / (rj * rnj));
-              float dk = 0.0f, ndk = 0.0f;
-              if (!(dist >= r)) {
-                const float v = r - dist;
-                dk = (-2.0f * dn) * v;
-                ndk = ((-3.0f * ndn) * v) * v;
-              }
-              fx = fx + (dirx * pt) * dk;
-              fy = fy + (diry * pt) * dk;
-              fx = fx + (dirx * npt) * ndk;
-              fy = fy + (diry * npt) * ndk;
-            }
+    for (int u = 0; u < kScanBatch; ++u) {
+      if (f + u < R.total && qi[u] != i) {
+        const float dx = q[u][0] - p[0], dy = q[u][1] - p[1];
+        const float sq = dx * dx + dy * dy;
+        if (!(sq > r2)) {
+          const float dist = sqrtf(sq);
+          float dirx, diry;
+          if (dist > 0.0001f) {
+            dirx = dx / dist;
+            diry = dy / dist;
+          } else {
+            dirx = 0.0f;
+            diry = 1.0f;
           }
+          const float pt = P_rho2 + q[u][2];    // + Pj / (rj * rj)
+          const float npt = Pn_rho2 + q[u][3];  // + Pnj / (rj * rnj)
+          float dk = 0.0f, ndk = 0.0f;
+          if (!(dist >= r)) {
+            const float v = r - dist;
+            dk = (-2.0f * dn) * v;
+            ndk = ((-3.0f * ndn) * v) * v;
+          }
+          fx = fx + (dirx * pt) * dk;
+          fy = fy + (diry * pt) * dk;
+          fx = fx + (dirx * npt) * ndk;
+          fy = fy + (diry * npt) * ndk;
         }
       }
-      if (stop) break;
     }
   }
-  float qx = own_dv[2] + fx * dt;  // post-gravity velocity (the pre pass, wgsl:397-400)
-  float qy = own_dv[3] + fy * dt;
+  const f4 own_pv = sl.rec_pv[t];
+  float qx = own_pv[2] + fx * dt;  // post-gravity velocity (the pre pass, wgsl:397-400)
+  float qy = own_pv[3] + fy * dt;
   float wx = 0.0f, wy = 0.0f;
-  for (int o = 0; o < 9; ++o) {
-    const uint32_t key = keys[o];
-    for (uint32_t j = starts[o]; j < N; j += kScanBatch) {
-      uint4 e[kScanBatch];
-      f2 vj[kScanBatch];
+  for (uint32_t f = 0; f < R.total; f += kScanBatch) {
+    f4 q[kScanBatch];
+    uint32_t qi[kScanBatch];
 #pragma unroll
-      for (int u = 0; u < kScanBatch; ++u) {
-        const uint32_t jj = min(j + u, N - 1u);
-        e[u] = rec_s[jj];
-        vj[u] = reinterpret_cast<const f2*>(dv_s)[2 * jj + 1];
-      }
-      bool stop = false;
+    for (int u = 0; u < kScanBatch; ++u) {
+      const uint32_t j = run_slot(R, min(f + u, R.total - 1u));
+      q[u] = sl.rec_pv[j];
+      qi[u] = sl.idx_s[j];
+    }
 #pragma unroll
-      for (int u = 0; u < kScanBatch; ++u) {
-        if (!stop) {
-          if (j + u >= N || e[u].x != key) {
-            stop = true;
-          } else if (e[u].y != i) {
-            const float dx = p[0] - __uint_as_float(e[u].z), dy = p[1] - __uint_as_float(e[u].w);
-            const float sq = dx * dx + dy * dy;
-            if (!(sq > r2)) {
-              const float dist = sqrtf(sq);
-              float k = 0.0f;
-              if (!(dist >= r)) {
-                const float v = r * r - dist * dist;
-                k = ((vn * v) * v) * v;
-              }
-              wx = wx + (vj[u][0] - qx) * k;
-              wy = wy + (vj[u][1] - qy) * k;
-            }
+    for (int u = 0; u < kScanBatch; ++u) {
+      if (f + u < R.total && qi[u] != i) {
+        const float dx = p[0] - q[u][0], dy = p[1] - q[u][1];
+        const float sq = dx * dx + dy * dy;
+        if (!(sq > r2)) {
+          const float dist = sqrtf(sq);
+          float k = 0.0f;
+          if (!(dist >= r)) {
+            const float v = r * r - dist * dist;
+            k = ((vn * v) * v) * v;
           }
+          wx = wx + (q[u][2] - qx) * k;
+          wy = wy + (q[u][3] - qy) * k;
         }
       }
-      if (stop) break;
     }
   }
   qx = qx + (wx * cfg->viscocity_strength) * dt;
   qy = qy + (wy * cfg->viscocity_strength) * dt;
-  float ox = x[i] + qx * dt;
-  float oy = y[i] + qy * dt;
+  const f2 c = sl.cur_s[t];
+  float ox = c[0] + qx * dt;
+  float oy = c[1] + qy * dt;
   wall(cfg->screen_bounds[0], cfg->screen_bounds[1], cfg->screen_bounds[2], cfg->screen_bounds[3],
        cfg->damping_factor, ox, oy, qx, qy);
-  x2[i] = ox;
-  y2[i] = oy;
-  vx2[i] = qx;
-  vy2[i] = qy;
+  st2[i] = f4{ox, oy, qx, qy};
+}
+
+// predicted_positions / densities (wgsl:58, :61) rebuilt from the slot records for
+// rps_read_debug: slot t holds particle idx_s[t]'s values (pads repeat identical ones).
+__global__ __launch_bounds__(kBlock) void sph_debug_views_kernel(SphSlots sl, f2* __restrict__ pred,
+                                                                 f2* __restrict__ dens,
+                                                                 uint32_t p_slots) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= p_slots) return;
+  const uint32_t i = sl.idx_s[t];
+  pred[i] = sl.pp_s[t];
+  dens[i] = sl.dens_s[t];
 }
 
 inline uint32_t blocks_for(uint64_t n, uint32_t per_block = kBlock) {
@@ -1199,8 +1207,8 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
     const int k = v && *v ? std::atoi(v) : 2;  // measured best
     return k < 1 ? 1 : (k > 3 ? 3 : k);
   }();
-  const SortBin bin{b.cfg, b.x, b.y, b.offsets, b.n};
-  const SortBin nobin{nullptr, nullptr, nullptr, nullptr, 0u};
+  const SortBin bin{b.cfg, b.st, b.offsets, b.n};
+  const SortBin nobin{nullptr, nullptr, nullptr, 0u};
   if (stages == 0) {  // P == 1: nothing to sort, only bin
     hipLaunchKernelGGL((sph_sort_local_kernel<true, 1>), dim3(1), dim3(64), 0, s, b.lookup, 1u, 1u, 0u,
                        0u, bin);
@@ -1252,39 +1260,52 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
 
 hipError_t launch_sph_offsets(const SphBuffers& b, hipStream_t s) {
   hipLaunchKernelGGL(sph_offsets_kernel, dim3(blocks_for(b.n)), dim3(kBlock), 0, s, b.lookup,
-                     b.offsets, b.n);
+                     b.offsets, b.ends, b.n);
   return hipGetLastError();
 }
 
 static int sph_batch() {
   static const int b = [] {
     const char* v = std::getenv("RPS_SPH_BATCH");
-    return v && *v && std::atoi(v) == 8 ? 8 : 4;
+    const int k = v && *v ? std::atoi(v) : 8;
+    return k == 4 || k == 16 ? k : 8;
   }();
   return b;
 }
 
 hipError_t launch_sph_pre(const SphBuffers& b, hipStream_t s) {
   hipLaunchKernelGGL(sph_predict_kernel, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg, b.lookup,
-                     b.x, b.y, b.vx, b.vy, b.pred, b.rec_s, b.dv_s, b.p);
+                     b.st, b.sl, b.p);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  if (sph_batch() == 8)
-    hipLaunchKernelGGL(sph_density_kernel<8>, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg,
-                       b.offsets, b.rec_s, b.dens, b.dv_s, b.p);
-  else
-    hipLaunchKernelGGL(sph_density_kernel<4>, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg,
-                       b.offsets, b.rec_s, b.dens, b.dv_s, b.p);
+#define RPS_DENSITY(B)                                                                           \
+  hipLaunchKernelGGL(sph_density_kernel<B>, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg, \
+                     b.offsets, b.ends, b.sl, b.p)
+  switch (sph_batch()) {
+    case 4: RPS_DENSITY(4); break;
+    case 16: RPS_DENSITY(16); break;
+    default: RPS_DENSITY(8); break;
+  }
+#undef RPS_DENSITY
   return hipGetLastError();
 }
 
 hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s) {
-  if (sph_batch() == 8)
-    hipLaunchKernelGGL(sph_sim_kernel<8>, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg,
-                       b.offsets, b.rec_s, b.dv_s, b.x, b.y, b.vx2, b.vy2, b.x2, b.y2, b.p);
-  else
-    hipLaunchKernelGGL(sph_sim_kernel<4>, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg,
-                       b.offsets, b.rec_s, b.dv_s, b.x, b.y, b.vx2, b.vy2, b.x2, b.y2, b.p);
+#define RPS_SIM(B)                                                                           \
+  hipLaunchKernelGGL(sph_sim_kernel<B>, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg, \
+                     b.offsets, b.ends, b.sl, b.st2, b.p)
+  switch (sph_batch()) {
+    case 4: RPS_SIM(4); break;
+    case 16: RPS_SIM(16); break;
+    default: RPS_SIM(8); break;
+  }
+#undef RPS_SIM
+  return hipGetLastError();
+}
+
+hipError_t launch_sph_debug_views(const SphBuffers& b, hipStream_t s) {
+  hipLaunchKernelGGL(sph_debug_views_kernel, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.sl,
+                     b.pred, b.dens, b.p);
   return hipGetLastError();
 }
 

@@ -69,15 +69,24 @@ def copy_soa(s):
 
 
 def assert_bitwise(a, b, what=""):
-    a = np.ascontiguousarray(a)
-    b = np.ascontiguousarray(b)
+    """Bit-for-bit equality; for f32, any NaN equals any NaN.  IEEE 754 (and WGSL) leave NaN
+    payloads and signs unspecified: the GPU's generated NaN is 0x7fc00000, x86's 0xffc00000,
+    and a negate modifier flips a propagated NaN's sign on one side and not the other.  No
+    non-NaN value on the path depends on a payload (comparisons, i32 casts and |v| ignore it),
+    so every non-NaN bit still has to match."""
+    a = np.ascontiguousarray(a).reshape(-1)
+    b = np.ascontiguousarray(b).reshape(-1)
     assert a.shape == b.shape, (what, a.shape, b.shape)
     ia = a.view(np.uint32) if a.dtype == np.float32 else a
     ib = b.view(np.uint32) if b.dtype == np.float32 else b
-    bad = np.nonzero(ia != ib)[0]
+    diff = ia != ib
+    if a.dtype == np.float32:
+        diff &= ~(np.isnan(a) & np.isnan(b))
+    bad = np.nonzero(diff)[0]
     if len(bad):
         i = bad[0]
-        raise AssertionError(f"{what}: {len(bad)} of {a.size} differ; first at {i}: {a.flat[i]!r} vs {b.flat[i]!r}")
+        raise AssertionError(f"{what}: {len(bad)} of {a.size} differ; first at {i}: {a[i]!r} ({ia[i]:#010x}) "
+                             f"vs {b[i]!r} ({ib[i]:#010x})")
 
 
 def assert_soa_bitwise(a, b, keys=("x", "y", "vx", "vy"), what=""):

@@ -19,7 +19,7 @@ run() {
 for step in "$@"; do
   case "$step" in
     tests)
-      run pytest_gpu 900 python -m pytest tests -m gpu -q -rf --durations=15; rc=$?
+      run pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf --durations=15 --timeout 300 --timeout-method thread; rc=$?
       [ $rc -le 1 ] || exit $rc ;;
     smoke)
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
@@ -36,14 +36,18 @@ for step in "$@"; do
       run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 40 --warmup 10 --no-cpu-baseline --allpairs-n 0 || exit $? ;;
     prof_sph)
       run prof_sph 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_sph -o run --output-format csv -- python3 tools/sph_frames.py 50000 60 || exit $? ;;
+    prof_sph:*)
+      n=${step#prof_sph:}
+      run prof_sph_$n 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_sph_$n -o run --output-format csv -- python3 tools/sph_frames.py $n 60 || exit $? ;;
     prof_sph64k)
       run prof_sph64k 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_sph64k -o run --output-format csv -- python3 tools/sph_frames.py 65536 60 || exit $? ;;
     probe)
       run hbm_probe 300 tools/hbm_probe || exit $? ;;
     *)
-      # arbitrary python script under tools/: "py:tools/foo.py"
+      # arbitrary python script under tools/: "py:tools/foo.py[,arg1,arg2...]"
       if [[ "$step" == py:* ]]; then
-        run "$(basename "${step#py:}" .py)" 900 python "${step#py:}" || exit $?
+        IFS=, read -r -a pyargs <<< "${step#py:}"
+        run "$(basename "${pyargs[0]}" .py)" 900 python "${pyargs[@]}" || exit $?
       else
         echo "unknown step $step"; exit 2
       fi ;;
