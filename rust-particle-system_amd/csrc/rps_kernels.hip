@@ -745,23 +745,22 @@ __global__ __launch_bounds__(kBlock) void sph_predict_kernel(const rps_config* _
 }
 
 // The nine runs a particle at predicted position p scans, in the reference's cell order
-// (wgsl:223-224 / :277-278), flattened: entry f (0 <= f < total) of the concatenation is
-// slot f + adj[o] for the cell o with cum[o] <= f < cum[o+1].  The 18 offsets/ends loads
-// are issued together.  A key absent from [0, N) has offsets 0xFFFFFFFF: an empty run.
-struct NineRuns {
-  uint32_t cum[9];  // entries before cell o
-  uint32_t adj[9];  // slot - flat index inside cell o (mod 2^32)
-  uint32_t total;
-};
+// (wgsl:223-224 / :277-278), flattened: entry f (0 <= f < total) of their concatenation.
+// The non-empty runs go to a per-lane LDS table, entry k = {slot - f of the run's first
+// entry, f one past its last}, so walking the flat index costs a compare per entry and an
+// LDS read per run boundary (RunCursor).  The 18 offsets/ends loads are issued together; a
+// key absent from [0, N) has offsets 0xFFFFFFFF, an empty run.
+typedef uint2 RunTable[9][kBlock];  // [run][lane]: consecutive lanes, consecutive banks
 
 __device__ __forceinline__ uint32_t grid_key(int32_t cx, int32_t cy, int o, uint32_t N) {
   return cell_key((int32_t)((uint32_t)cx + (uint32_t)kGridOff[o][0]),
                   (int32_t)((uint32_t)cy + (uint32_t)kGridOff[o][1]), N);
 }
 
-__device__ __forceinline__ NineRuns nine_runs(const uint32_t* __restrict__ offsets,
+__device__ __forceinline__ uint32_t nine_runs(const uint32_t* __restrict__ offsets,
                                               const uint32_t* __restrict__ ends, float px, float py,
-                                              float xoff, float yoff, float r, uint32_t N) {
+                                              float xoff, float yoff, float r, uint32_t N,
+                                              RunTable& runs) {
   const int32_t cx = f32_to_i32((px + xoff) / r);  // particle_position_to_cell_coord, wgsl:121-130
   const int32_t cy = f32_to_i32((py + yoff) / r);
   uint32_t key[9], s[9], e[9];
@@ -772,27 +771,29 @@ __device__ __forceinline__ NineRuns nine_runs(const uint32_t* __restrict__ offse
     s[o] = offsets[key[o]];
     e[o] = ends[key[o]];
   }
-  NineRuns R;
-  uint32_t c = 0;
+  uint32_t c = 0, m = 0;
 #pragma unroll
   for (int o = 0; o < 9; ++o) {
-    const uint32_t len = s[o] < N ? e[o] - s[o] : 0u;
-    R.cum[o] = c;
-    R.adj[o] = s[o] - c;
-    c += len;
+    if (s[o] < N) {
+      runs[m][threadIdx.x] = make_uint2(s[o] - c, c + (e[o] - s[o]));
+      c += e[o] - s[o];
+      ++m;
+    }
   }
-  R.total = c;
-  return R;
+  return c;
 }
 
-// Slot of flat entry f (f < total): the last cell whose run starts at or before f.  Cells
-// with empty runs share their successor's cum and are skipped by the >= chain.
-__device__ __forceinline__ uint32_t run_slot(const NineRuns& R, uint32_t f) {
-  uint32_t j = f + R.adj[0];
-#pragma unroll
-  for (int o = 1; o < 9; ++o) j = f >= R.cum[o] ? f + R.adj[o] : j;
-  return j;
-}
+// Walks the flat index forward: slot(f) for non-decreasing f < total.
+struct RunCursor {
+  const RunTable& runs;
+  uint32_t r = 0;
+  uint2 cur;
+  __device__ explicit RunCursor(const RunTable& t) : runs(t), cur(t[0][threadIdx.x]) {}
+  __device__ __forceinline__ uint32_t slot(uint32_t f) {
+    if (f >= cur.y) cur = runs[++r][threadIdx.x];  // runs are non-empty: one step suffices
+    return f + cur.x;
+  }
+};
 
 // Work mapping of the density and sim passes: thread t takes lookup slot t of all P.  Lanes
 // of a wave then hold the particles of a few cells and read the same runs together.  Every
@@ -813,17 +814,18 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
   const float r = cfg->smoothing_radius, r2 = r * r;
   const uint32_t N = cfg->particle_count;
   const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
-  const NineRuns R = nine_runs(offsets, ends, p[0], p[1], cfg->screen_bounds[1],
-                               cfg->screen_bounds[3], r, N);
+  __shared__ RunTable runs;
+  const uint32_t total = nine_runs(offsets, ends, p[0], p[1], cfg->screen_bounds[1],
+                                   cfg->screen_bounds[3], r, N, runs);
+  RunCursor rc(runs);
   float d = 0.0f, nd = 0.0f;
-  for (uint32_t f = 0; f < R.total; f += kScanBatch) {
+  for (uint32_t f = 0; f < total; f += kScanBatch) {
     f2 q[kScanBatch];
 #pragma unroll
-    for (int u = 0; u < kScanBatch; ++u)
-      q[u] = sl.pp_s[run_slot(R, min(f + u, R.total - 1u))];
+    for (int u = 0; u < kScanBatch; ++u) q[u] = sl.pp_s[rc.slot(min(f + u, total - 1u))];
 #pragma unroll
     for (int u = 0; u < kScanBatch; ++u) {
-      if (f + u < R.total) {
+      if (f + u < total) {
         const float dx = p[0] - q[u][0], dy = p[1] - q[u][1];
         const float sq = dx * dx + dy * dy;
         if (!(sq > r2)) {
@@ -873,21 +875,23 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
   const float Pn = own_d[1] * cfg->near_density_multiplier;
   const float P_rho2 = own[2];             // loop-invariant halves of pressure_term and
   const float Pn_rho2 = Pn / (rho * rho);  // near_pressure_term (wgsl:323-327)
-  const NineRuns R = nine_runs(offsets, ends, p[0], p[1], cfg->screen_bounds[1],
-                               cfg->screen_bounds[3], r, N);
+  __shared__ RunTable runs;
+  const uint32_t total = nine_runs(offsets, ends, p[0], p[1], cfg->screen_bounds[1],
+                                   cfg->screen_bounds[3], r, N, runs);
   float fx = 0.0f, fy = 0.0f;
-  for (uint32_t f = 0; f < R.total; f += kScanBatch) {
+  RunCursor rc(runs);
+  for (uint32_t f = 0; f < total; f += kScanBatch) {
     f4 q[kScanBatch];
     uint32_t qi[kScanBatch];
 #pragma unroll
     for (int u = 0; u < kScanBatch; ++u) {
-      const uint32_t j = run_slot(R, min(f + u, R.total - 1u));
+      const uint32_t j = rc.slot(min(f + u, total - 1u));
       q[u] = sl.rec_pd[j];
       qi[u] = sl.idx_s[j];
     }
 #pragma unroll
     for (int u = 0; u < kScanBatch; ++u) {
-      if (f + u < R.total && qi[u] != i) {
+      if (f + u < total && qi[u] != i) {
         const float dx = q[u][0] - p[0], dy = q[u][1] - p[1];
         const float sq = dx * dx + dy * dy;
         if (!(sq > r2)) {
@@ -920,18 +924,19 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
   float qx = own_pv[2] + fx * dt;  // post-gravity velocity (the pre pass, wgsl:397-400)
   float qy = own_pv[3] + fy * dt;
   float wx = 0.0f, wy = 0.0f;
-  for (uint32_t f = 0; f < R.total; f += kScanBatch) {
+  RunCursor rc2(runs);
+  for (uint32_t f = 0; f < total; f += kScanBatch) {
     f4 q[kScanBatch];
     uint32_t qi[kScanBatch];
 #pragma unroll
     for (int u = 0; u < kScanBatch; ++u) {
-      const uint32_t j = run_slot(R, min(f + u, R.total - 1u));
+      const uint32_t j = rc2.slot(min(f + u, total - 1u));
       q[u] = sl.rec_pv[j];
       qi[u] = sl.idx_s[j];
     }
 #pragma unroll
     for (int u = 0; u < kScanBatch; ++u) {
-      if (f + u < R.total && qi[u] != i) {
+      if (f + u < total && qi[u] != i) {
         const float dx = p[0] - q[u][0], dy = p[1] - q[u][1];
         const float sq = dx * dx + dy * dy;
         if (!(sq > r2)) {
