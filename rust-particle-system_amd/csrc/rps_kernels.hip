@@ -562,7 +562,7 @@ __global__ __launch_bounds__(kBlock) void nbody_integrate_kernel(NbodyIntegrateA
 // network, the same comparisons, so the same result as K pass-per-dispatch launches.
 // `mem` is the lookup (global passes) or the workgroup's LDS tile (local passes).
 template <int K, bool FLIP, class T>
-__device__ __forceinline__ void sort_group(T* mem, uint32_t base, uint32_t r, uint32_t g) {
+__device__ __forceinline__ void sort_group(T mem, uint32_t base, uint32_t r, uint32_t g) {
   constexpr int M = 1 << K;            // entries per residue class
   constexpr int E = FLIP ? 2 * M : M;  // entries per group
   uint2 v[E];
@@ -628,6 +628,14 @@ __global__ __launch_bounds__(kBlock) void sph_sort_fused_kernel(uint2* __restric
 }
 
 constexpr uint32_t kSortTile = 8192;  // entries per workgroup tile (64 KiB of LDS)
+
+// LDS view of a sort tile with one pad entry per 32 (256 B, one pass over the 64 banks):
+// the small-stride passes have lanes 16-32 B apart, which without padding land on 8 of the
+// 32 bank pairs (8-way conflicts); padded they spread over all 32.
+struct PaddedTile {
+  uint2* p;
+  __device__ __forceinline__ uint2& operator[](uint32_t i) const { return p[i + (i >> 5)]; }
+};
 constexpr uint32_t kSortFuse = 4;     // global passes per register-fused launch
 
 // bin_particles_in_grid (wgsl:455-468) folded into the first sort launch: entries [0, n)
@@ -649,49 +657,88 @@ __device__ __forceinline__ uint2 bin_entry(const SortBin& b, uint32_t i) {
   return make_uint2(cell_key(cx, cy, b.cfg->particle_count), i);
 }
 
+// One register chunk of the passes of `stage` starting at `step` (sort_group: up to KMAX
+// passes, flip first: up to KMAX-1) over the `len` entries at `off` of the tile, groups dealt
+// to work-items w0, w0 + wn, ...  Returns the number of passes covered.
+template <int KMAX>
+__device__ __forceinline__ uint32_t sort_chunk(const PaddedTile& s, uint32_t off, uint32_t len,
+                                               uint32_t stage, uint32_t step, uint32_t w0,
+                                               uint32_t wn) {
+  const uint32_t G = 1u << (stage - step);
+  const uint32_t left = stage - step + 1u;  // passes left in this stage
+  // A flip pass with G = 1 pairs (2i, 2i+1) exactly like a non-flip one.
+  const bool flip = step == 0u && G > 1u;
+  const uint32_t kf = KMAX > 1 ? (uint32_t)KMAX - 1u : 1u;  // flip chunks: 2^(K+1) entries
+  const uint32_t K = flip ? (G >= (2u << (kf - 1u)) ? kf : 1u)
+                          : (left < (uint32_t)KMAX ? left : (uint32_t)KMAX);
+  const uint32_t g = G >> (K - 1u);
+  const uint32_t groups = sort_groups(len, G, g, flip);
+  for (uint32_t q = w0; q < groups; q += wn) {
+    uint32_t b, r;
+    sort_group_at(q, G, g, flip, b, r);
+    if (flip) {
+      if (KMAX >= 3 && K == 2u) sort_group<2, true>(s, off + b, r, g);
+      else sort_group<1, true>(s, off + b, r, g);
+    } else {
+      if (KMAX >= 3 && K == 3u) sort_group<3, false>(s, off + b, r, g);
+      else if (KMAX >= 2 && K == 2u) sort_group<2, false>(s, off + b, r, g);
+      else sort_group<1, false>(s, off + b, r, g);
+    }
+  }
+  return K;
+}
+
+// A wave's LDS writes visible to its own later LDS reads (any lane): LDS serves one wave's
+// instructions in order; the wait and the wavefront fences keep the compiler from moving
+// LDS accesses across the point.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Every remaining pass of stages [stage_lo, stage_hi] whose group_width fits one tile:
 // a pass with 2*gw <= tile only pairs entries inside aligned blocks of 2*gw, so a tile of
-// the array can run it on its own.  Passes go in register chunks (sort_group) of up to 3
-// (flip first: up to 2) per barrier; same network, same compare order per pair -> identical
-// result to the reference's pass-per-dispatch schedule.
+// the array can run it on its own.  Passes go in register chunks (sort_group) of up to KMAX
+// (flip first: up to KMAX-1).  Passes whose span 2*gw exceeds a wave's share of the tile
+// (64 lanes x one group each) run across the workgroup with a barrier per chunk; the rest
+// -- every pass of the early stages and the tail of each later stage -- run inside each
+// wave's own span with only wave-level ordering.  Same network, same compare order per pair
+// -> identical result to the reference's pass-per-dispatch schedule.
 template <bool BIN, int KMAX>
 __global__ __launch_bounds__(1024) void sph_sort_local_kernel(
     uint2* __restrict__ lookup, uint32_t tile, uint32_t stage_lo, uint32_t stage_hi,
     uint32_t first_step, SortBin bin) {
-  __shared__ uint2 s[kSortTile];
+  __shared__ uint2 lds[kSortTile + kSortTile / 32];
+  const PaddedTile s{lds};
   const uint32_t base0 = blockIdx.x * tile;
   for (uint32_t q = threadIdx.x; q < tile; q += blockDim.x) {
     const uint32_t gq = base0 + q;
     s[q] = (BIN && gq < bin.n) ? bin_entry(bin, gq) : lookup[gq];
   }
   __syncthreads();
-  for (uint32_t stage = stage_lo; stage <= stage_hi; ++stage) {
-    uint32_t step = stage == stage_lo ? first_step : 0u;
-    while (step <= stage) {
-      const uint32_t G = 1u << (stage - step);
-      const uint32_t left = stage - step + 1u;  // passes left in this stage
-      // A flip pass with G = 1 pairs (2i, 2i+1) exactly like a non-flip one.
-      const bool flip = step == 0u && G > 1u;
-      const uint32_t kf = KMAX > 1 ? (uint32_t)KMAX - 1u : 1u;  // flip chunks: 2^(K+1) entries
-      const uint32_t K = flip ? (G >= (2u << (kf - 1u)) ? kf : 1u)
-                              : (left < (uint32_t)KMAX ? left : (uint32_t)KMAX);
-      const uint32_t g = G >> (K - 1u);
-      const uint32_t groups = sort_groups(tile, G, g, flip);
-      for (uint32_t q = threadIdx.x; q < groups; q += blockDim.x) {
-        uint32_t b, r;
-        sort_group_at(q, G, g, flip, b, r);
-        if (flip) {
-          if (KMAX >= 3 && K == 2u) sort_group<2, true>(s, b, r, g);
-          else sort_group<1, true>(s, b, r, g);
-        } else {
-          if (KMAX >= 3 && K == 3u) sort_group<3, false>(s, b, r, g);
-          else if (KMAX >= 2 && K == 2u) sort_group<2, false>(s, b, r, g);
-          else sort_group<1, false>(s, b, r, g);
+  const uint32_t ws = min(tile, 64u << KMAX);  // one wave's span (blockDim is a multiple of 64)
+  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  uint32_t stage = stage_lo, step = first_step;
+  while (stage <= stage_hi) {
+    while (step <= stage && (2u << (stage - step)) > ws) {  // cross-wave passes
+      step += sort_chunk<KMAX>(s, 0u, tile, stage, step, threadIdx.x, blockDim.x);
+      __syncthreads();
+    }
+    uint32_t last = stage;  // later stages whose whole network is wave-local join in
+    while (last < stage_hi && (2u << (last + 1u)) <= ws) ++last;
+    for (uint32_t reg = wid; reg < tile / ws; reg += nw) {
+      for (uint32_t st = stage, sp = step; st <= last; ++st, sp = 0u) {
+        while (sp <= st) {
+          sp += sort_chunk<KMAX>(s, reg * ws, ws, st, sp, lane, 64u);
+          wave_lds_sync();
         }
       }
-      __syncthreads();
-      step += K;
     }
+    __syncthreads();
+    stage = last + 1u;
+    step = 0u;
   }
   for (uint32_t q = threadIdx.x; q < tile; q += blockDim.x) lookup[base0 + q] = s[q];
 }
@@ -1207,10 +1254,10 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
   while ((1u << stages) < P) ++stages;
   *passes = stages * (stages + 1u) / 2u;
   *launches = 0;
-  static const int kmax = [] {
+  static const int kmax_env = [] {
     const char* v = std::getenv("RPS_SORT_KMAX");
-    const int k = v && *v ? std::atoi(v) : 2;  // measured best
-    return k < 1 ? 1 : (k > 3 ? 3 : k);
+    const int k = v && *v ? std::atoi(v) : 0;  // 0: by tile size (below)
+    return k < 0 ? 0 : (k > 3 ? 3 : k);
   }();
   const SortBin bin{b.cfg, b.st, b.offsets, b.n};
   const SortBin nobin{nullptr, nullptr, nullptr, 0u};
@@ -1224,6 +1271,9 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
   // passes), 8192 above (fewer global passes; measured at 50 k / 1 M / 4 M particles).
   const uint32_t want = P <= (1u << 18) ? 2048u : kSortTile;  // 1024/4096/8192 measured slower
   const uint32_t tile = P < want ? P : want;
+  // Passes per register chunk: 3 on 8192-entry tiles, 2 on smaller ones (measured at 65 536,
+  // 2^20 and 2^22 particles).
+  const int kmax = kmax_env ? kmax_env : (tile >= kSortTile ? 3 : 2);
   uint32_t tile_log = 0;
   while ((1u << tile_log) < tile) ++tile_log;
   const uint32_t tiles = P / tile;
