@@ -901,7 +901,10 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
 // simulation_step, compute_shader.wgsl:435-453: pressure (:256-334) and viscosity
 // (:336-384) against the start-of-pass velocity snapshot (rec_pv.zw), Euler (:392-395) and
 // walls (:69-99).  The new packed state of particle i goes to st2[i].
-template <int kScanBatch>
+// Self-skip (wgsl:295, :365) compares particle indices.  With P == N there are no pad entries,
+// every particle owns exactly one slot, and the index test is the slot test j != t: that
+// saves the 4-B index load per scanned entry (kPads = false).
+template <int kScanBatch, bool kPads>
 __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __restrict__ cfg,
                                                          const uint32_t* __restrict__ offsets,
                                                          const uint32_t* __restrict__ ends,
@@ -912,6 +915,7 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
   const f4 own = sl.rec_pd[t];  // own predicted position (xy) and P / rho^2 (z)
   const f2 own_d = sl.dens_s[t];
   const uint32_t i = sl.idx_s[t];
+  const uint32_t self = kPads ? i : t;
   const float dt = cfg->fixed_delta_time;
   const float r = cfg->smoothing_radius, r2 = r * r;
   const uint32_t N = cfg->particle_count;
@@ -934,11 +938,11 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
     for (int u = 0; u < kScanBatch; ++u) {
       const uint32_t j = rc.slot(min(f + u, total - 1u));
       q[u] = sl.rec_pd[j];
-      qi[u] = sl.idx_s[j];
+      qi[u] = kPads ? sl.idx_s[j] : j;
     }
 #pragma unroll
     for (int u = 0; u < kScanBatch; ++u) {
-      if (f + u < total && qi[u] != i) {
+      if (f + u < total && qi[u] != self) {
         const float dx = q[u][0] - p[0], dy = q[u][1] - p[1];
         const float sq = dx * dx + dy * dy;
         if (!(sq > r2)) {
@@ -979,11 +983,11 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
     for (int u = 0; u < kScanBatch; ++u) {
       const uint32_t j = rc2.slot(min(f + u, total - 1u));
       q[u] = sl.rec_pv[j];
-      qi[u] = sl.idx_s[j];
+      qi[u] = kPads ? sl.idx_s[j] : j;
     }
 #pragma unroll
     for (int u = 0; u < kScanBatch; ++u) {
-      if (f + u < total && qi[u] != i) {
+      if (f + u < total && qi[u] != self) {
         const float dx = p[0] - q[u][0], dy = p[1] - q[u][1];
         const float sq = dx * dx + dy * dy;
         if (!(sq > r2)) {
@@ -1346,9 +1350,13 @@ hipError_t launch_sph_pre(const SphBuffers& b, hipStream_t s) {
 }
 
 hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s) {
-#define RPS_SIM(B)                                                                           \
-  hipLaunchKernelGGL(sph_sim_kernel<B>, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg, \
-                     b.offsets, b.ends, b.sl, b.st2, b.p)
+#define RPS_SIM(B)                                                                              \
+  if (b.p == b.n)                                                                              \
+    hipLaunchKernelGGL((sph_sim_kernel<B, false>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s,  \
+                       b.cfg, b.offsets, b.ends, b.sl, b.st2, b.p);                            \
+  else                                                                                         \
+    hipLaunchKernelGGL((sph_sim_kernel<B, true>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s,   \
+                       b.cfg, b.offsets, b.ends, b.sl, b.st2, b.p)
   switch (sph_batch()) {
     case 4: RPS_SIM(4); break;
     case 16: RPS_SIM(16); break;
