@@ -627,7 +627,8 @@ __global__ __launch_bounds__(kBlock) void sph_sort_fused_kernel(uint2* __restric
   sort_group<K, FLIP>(lookup, base, r, g);
 }
 
-constexpr uint32_t kSortTile = 8192;  // entries per workgroup tile (64 KiB of LDS)
+constexpr uint32_t kSortTile = 8192;      // entries per workgroup tile (64 KiB of LDS)
+constexpr uint32_t kSortTileMax = 16384;  // largest tile (132 KiB of LDS, one workgroup per CU)
 
 // LDS view of a sort tile with one pad entry per 32 (256 B, one pass over the 64 banks):
 // the small-stride passes have lanes 16-32 B apart, which without padding land on 8 of the
@@ -636,7 +637,6 @@ struct PaddedTile {
   uint2* p;
   __device__ __forceinline__ uint2& operator[](uint32_t i) const { return p[i + (i >> 5)]; }
 };
-constexpr uint32_t kSortFuse = 4;     // global passes per register-fused launch
 
 // bin_particles_in_grid (wgsl:455-468) folded into the first sort launch: entries [0, n)
 // get (key, i) from the current positions and offsets[i] <- 0xFFFFFFFF; entries [n, P) keep
@@ -706,11 +706,11 @@ __device__ __forceinline__ void wave_lds_sync() {
 // -- every pass of the early stages and the tail of each later stage -- run inside each
 // wave's own span with only wave-level ordering.  Same network, same compare order per pair
 // -> identical result to the reference's pass-per-dispatch schedule.
-template <bool BIN, int KMAX>
+template <bool BIN, int KMAX, uint32_t CAP = kSortTile>
 __global__ __launch_bounds__(1024) void sph_sort_local_kernel(
     uint2* __restrict__ lookup, uint32_t tile, uint32_t stage_lo, uint32_t stage_hi,
     uint32_t first_step, SortBin bin) {
-  __shared__ uint2 lds[kSortTile + kSortTile / 32];
+  __shared__ uint2 lds[CAP + CAP / 32];
   const PaddedTile s{lds};
   const uint32_t base0 = blockIdx.x * tile;
   for (uint32_t q = threadIdx.x; q < tile; q += blockDim.x) {
@@ -1235,8 +1235,13 @@ static hipError_t launch_sort_fused(uint2* lookup, uint32_t P, uint32_t G, bool 
 static hipError_t launch_sort_local(int kmax, bool bin, uint32_t tiles, uint32_t threads,
                                     hipStream_t s, uint2* lookup, uint32_t tile, uint32_t lo,
                                     uint32_t hi, uint32_t first, const SortBin& sb) {
-#define RPS_LOCAL(B, K) \
-  hipLaunchKernelGGL((sph_sort_local_kernel<B, K>), dim3(tiles), dim3(threads), 0, s, lookup, tile, lo, hi, first, sb)
+#define RPS_LOCAL(B, K)                                                                          \
+  if (tile > kSortTile)                                                                          \
+    hipLaunchKernelGGL((sph_sort_local_kernel<B, K, kSortTileMax>), dim3(tiles), dim3(threads), 0, \
+                       s, lookup, tile, lo, hi, first, sb);                                      \
+  else                                                                                           \
+    hipLaunchKernelGGL((sph_sort_local_kernel<B, K>), dim3(tiles), dim3(threads), 0, s, lookup,  \
+                       tile, lo, hi, first, sb)
   if (bin) {
     if (kmax == 3) RPS_LOCAL(true, 3);
     else if (kmax == 2) RPS_LOCAL(true, 2);
@@ -1273,7 +1278,17 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
   }
   // Tile: 2048 entries up to P = 2^18 (enough workgroups to fill the chip in the LDS
   // passes), 8192 above (fewer global passes; measured at 50 k / 1 M / 4 M particles).
-  const uint32_t want = P <= (1u << 18) ? 2048u : kSortTile;  // 1024/4096/8192 measured slower
+  static const uint32_t tile_env = [] {
+    const char* v = std::getenv("RPS_SORT_TILE");
+    const uint32_t t = v && *v ? (uint32_t)std::atoi(v) : 0u;
+    return (t >= 64u && t <= kSortTileMax && (t & (t - 1u)) == 0u) ? t : 0u;
+  }();
+  static const uint32_t fuse = [] {
+    const char* v = std::getenv("RPS_SORT_FUSE");
+    const int k = v && *v ? std::atoi(v) : 4;
+    return (uint32_t)(k < 1 ? 1 : (k > 5 ? 5 : k));
+  }();
+  const uint32_t want = tile_env ? tile_env : (P <= (1u << 18) ? 2048u : kSortTile);
   const uint32_t tile = P < want ? P : want;
   // Passes per register chunk: 3 on 8192-entry tiles, 2 on smaller ones (measured at 65 536,
   // 2^20 and 2^22 particles).
@@ -1290,19 +1305,20 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
   if (e != hipSuccess) return e;
   for (uint32_t stage = first_global_stage; stage < stages; ++stage) {
     // Passes whose compare span 2*gw exceeds the tile are global: steps [0, T).  They run
-    // in register-fused chunks of up to kSortFuse passes (sph_sort_fused_kernel).
+    // in register-fused chunks of up to `fuse` passes (sph_sort_fused_kernel).
     uint32_t T = 0;
     while (T <= stage && 2u * (1u << (stage - T)) > tile) ++T;
     uint32_t step = 0;
     while (step < T) {
-      const uint32_t k = T - step < kSortFuse ? T - step : kSortFuse;
+      const uint32_t k = T - step < fuse ? T - step : fuse;
       const uint32_t G = 1u << (stage - step);
       const bool flip = step == 0;
       switch (k) {
         case 1: e = launch_sort_fused<1>(b.lookup, P, G, flip, s); break;
         case 2: e = launch_sort_fused<2>(b.lookup, P, G, flip, s); break;
         case 3: e = launch_sort_fused<3>(b.lookup, P, G, flip, s); break;
-        default: e = launch_sort_fused<4>(b.lookup, P, G, flip, s); break;
+        case 4: e = launch_sort_fused<4>(b.lookup, P, G, flip, s); break;
+        default: e = launch_sort_fused<5>(b.lookup, P, G, flip, s); break;
       }
       ++*launches;
       if (e != hipSuccess) return e;
