@@ -6,8 +6,9 @@ moving on circles, drag, lifetime decay + Philox respawn, semi-implicit Euler, w
 "step" = one fused stream-kernel launch over every particle (in place, tiled SoA, 34 B per
 particle of algorithmic HBM traffic: x, y, vx, vy read+written, the u16 lifetime expiry
 read).  Multi-GPU: one process per GPU, contiguous index shards with global particle ids, no
-data-path collective (weak scaling: 1e8 particles per rank).  Side line "allpairs": the
-all-pairs N-body step with its RCCL all-gather, strong-scaled over the ranks.
+data-path collective (weak scaling: 1e8 particles per rank).  Side lines: "sph", the
+reference's five-pass SPH frame at 2^22 particles (replicas); "allpairs", the all-pairs
+N-body step with its RCCL all-gather, strong-scaled over the ranks.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
@@ -44,6 +45,9 @@ def parse():
     ap.add_argument("--allpairs-n", type=int, default=1 << 22,
                     help="global particles of the all-pairs N-body side measurement (0: skip)")
     ap.add_argument("--allpairs-steps", type=int, default=2)
+    ap.add_argument("--sph-n", type=int, default=1 << 22,
+                    help="particles of the SPH-frame side measurement per rank (0: skip)")
+    ap.add_argument("--sph-frames", type=int, default=50)
     ap.add_argument("--allpairs-timeout", type=float, default=240.0,
                     help="watchdog: print the headline line and exit if the side run hangs")
     return ap.parse_args()
@@ -181,6 +185,41 @@ def allpairs(rps, args, d):
             "collective": f"ncclAllGather {8 * ng} B per step" if d.world > 1 else "none (1 rank)"}
 
 
+def sph_side(rps, args, d):
+    """Side measurement: the reference's full five-pass SPH frame (bin,
+    bitonic sort, offsets, pre-simulation, simulation) at `sph_n` particles, the reference
+    scatter spread over a viewport scaled to keep the default density.  SPH does not shard in
+    this tier, so every rank runs its own replica; the aggregate is
+    replicas x particles x frames / max-over-ranks time."""
+    n = args.sph_n
+    scale = max(1.0, (n / 50000) ** 0.5)
+    cfg = rps.default_particle_config(n, screen_bounds=rps.screen_bounds_for(1920.0 * scale, 1080.0 * scale))
+    parts = rps.setup_particles_scatter(cfg, n, seed=args.seed)
+    ctx = rps.Context(n, rps.MODE_SPH, device=d.local if d.dist else 0)
+    try:
+        ctx.set_config(cfg, rps.make_ext(shader_delay=0))
+        ctx.upload(parts)
+        ctx.step(10)
+        ctx.sync()
+        d.sync_device()
+        d.barrier()
+        ctx.set_profiling(1)
+        t0 = time.perf_counter()
+        ctx.step(args.sph_frames)
+        ctx.sync()
+        d.sync_device()
+        t1 = time.perf_counter()
+        d.barrier()
+        el = d.max(t1 - t0)
+        sim_ms, _ = ctx.kernel_time()
+    finally:
+        ctx.close()
+    return {"workload": f"SPH frame (5 passes, bitwise == oracle), {n} particles per rank, reference scatter",
+            "scaling": "replicas", "frames": args.sph_frames, "ms_per_frame": el * 1e3 / args.sph_frames,
+            "particle_steps_per_s": float(n) * d.world * args.sph_frames / el,
+            "sim_kernel_ms": d.max(sim_ms)}
+
+
 def main():
     args = parse()
     d = Dist()
@@ -242,12 +281,15 @@ def main():
     }
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(rps, args, cfg, ext)
-    if args.allpairs_n > 0:
+    sides = [("sph", sph_side, args.sph_n > 0), ("allpairs", allpairs, args.allpairs_n > 0)]
+    for key, fn, on in sides:
+        if not on:
+            continue
         import threading
 
-        def _watchdog():  # a hung side run must not cost the headline line
+        def _watchdog(key=key):  # a hung side run must not cost the headline line
             if d.rank == 0:
-                line["allpairs"] = {"error": f"watchdog: no result within {args.allpairs_timeout} s"}
+                line[key] = {"error": f"watchdog: no result within {args.allpairs_timeout} s"}
                 print(json.dumps(line), flush=True)
             os._exit(0)
 
@@ -255,9 +297,9 @@ def main():
         timer.daemon = True
         timer.start()
         try:
-            line["allpairs"] = allpairs(rps, args, d)
+            line[key] = fn(rps, args, d)
         except Exception as ex:  # report, keep the headline
-            line["allpairs"] = {"error": f"{type(ex).__name__}: {ex}"}
+            line[key] = {"error": f"{type(ex).__name__}: {ex}"}
         timer.cancel()
     if d.rank == 0:
         print(json.dumps(line), flush=True)

@@ -32,8 +32,8 @@ for step in "$@"; do
     prof)
       run prof_trace 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace -o run --output-format csv -- python3 bench.py --no-cpu-baseline || exit $? ;;
     pmc)
-      run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 40 --warmup 10 --no-cpu-baseline --allpairs-n 0 || exit $?
-      run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 40 --warmup 10 --no-cpu-baseline --allpairs-n 0 || exit $? ;;
+      run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 40 --warmup 10 --no-cpu-baseline --allpairs-n 0 --sph-n 0 || exit $?
+      run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 40 --warmup 10 --no-cpu-baseline --allpairs-n 0 --sph-n 0 || exit $? ;;
     prof_sph)
       run prof_sph 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_sph -o run --output-format csv -- python3 tools/sph_frames.py 50000 60 || exit $? ;;
     prof_sph:*)
