@@ -91,6 +91,7 @@ struct SphSlots {
   f2* dens_s;    // P {density, near density}
   uint32_t* idx_s;  // P particle index (self-skip, wgsl:295 / :365)
   f2* cur_s;     // P current positions (Euler base)
+  uint64_t* nbr_mask;  // 2 x P: bit f set <=> flat entry f of the nine runs is within the radius
 };
 struct SphBuffers {
   const rps_config* cfg;  // device-resident ParticleConfig

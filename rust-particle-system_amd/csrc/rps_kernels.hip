@@ -840,6 +840,11 @@ struct RunCursor {
     if (f >= cur.y) cur = runs[++r][threadIdx.x];  // runs are non-empty: one step suffices
     return f + cur.x;
   }
+  // The same for increasing f that may skip whole runs.
+  __device__ __forceinline__ uint32_t slot_skip(uint32_t f) {
+    while (f >= cur.y) cur = runs[++r][threadIdx.x];
+    return f + cur.x;
+  }
 };
 
 // Work mapping of the density and sim passes: thread t takes lookup slot t of all P.  Lanes
@@ -847,6 +852,16 @@ struct RunCursor {
 // particle's fresh entry is in exactly one slot; pad slots repeat some
 // particle, whose recomputation writes the identical value (outputs are separate buffers),
 // so the race is benign and results are independent of it.
+//
+// Neighbour masks.  Only about a third of the 3x3-cell entries lie within the smoothing
+// radius; the reference adds nothing for the others (wgsl:246, :299-301, :369).  The
+// density pass, which tests every entry anyway, sets bit f of a 128-bit mask per slot for
+// each flat entry f within the radius (two u64 words, nbr_mask[w * P + t], one coalesced
+// store each).  The sim pass rebuilds the same run table and visits only the set bits, in
+// increasing f, for both of its scans: the wave pays the force bodies for the most entries
+// any lane has within the radius, not for every entry scanned.  The radius test is the same
+// on both sides: the sim's (q - p)^2 sums equal the density's (p - q)^2 sums bit for bit.
+// A particle with more than 128 entries in its nine runs scans and tests them as before.
 //
 // calculate_density, compute_shader.wgsl:207-254: entries summed in run order, kScanBatch
 // predicted positions in flight per lane across run boundaries.
@@ -866,6 +881,7 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
                                    cfg->screen_bounds[3], r, N, runs);
   RunCursor rc(runs);
   float d = 0.0f, nd = 0.0f;
+  uint64_t m0 = 0, m1 = 0;
   for (uint32_t f = 0; f < total; f += kScanBatch) {
     f2 q[kScanBatch];
 #pragma unroll
@@ -876,6 +892,11 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
         const float dx = p[0] - q[u][0], dy = p[1] - q[u][1];
         const float sq = dx * dx + dy * dy;
         if (!(sq > r2)) {
+          const uint32_t b = f + u;
+          if (total <= 128u) {  // otherwise the sim pass scans the runs (masks unused)
+            if (b < 64u) m0 |= 1ull << b;
+            else m1 |= 1ull << (b - 64u);
+          }
           const float dist = sqrtf(sq);
           float k1 = 0.0f, k2 = 0.0f;
           if (!(dist >= r)) {
@@ -889,6 +910,8 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
       }
     }
   }
+  sl.nbr_mask[t] = m0;
+  sl.nbr_mask[p_slots + t] = m1;
   // The neighbour halves of pressure_term / near_pressure_term (wgsl:323-327) depend on this
   // particle alone: evaluated once here (same ops, same bits) instead of per visiting
   // neighbour in the sim pass.
@@ -898,12 +921,71 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
   sl.dens_s[t] = f2{d, nd};
 }
 
+// Drivers of the sim pass's two scans: body(q) for every entry within the radius that is
+// not the particle itself, in the reference's order, q = load(slot).  Self-skip (wgsl:295,
+// :365) compares particle indices; with P == N there are no pad entries, every particle owns
+// exactly one slot, and the index test is the slot test j != t, which saves the 4-B index
+// load per entry (kPads = false).
+template <int kScanBatch, bool kPads, class Load, class Body>
+__device__ __forceinline__ void scan_masked(const SphSlots& sl, const RunTable& runs, uint64_t m0,
+                                            uint64_t m1, uint32_t self, Load&& load, Body&& body) {
+  RunCursor rc(runs);
+  while (m0 | m1) {
+    uint32_t fs[kScanBatch], qi[kScanBatch];
+    bool live[kScanBatch];
+    f4 q[kScanBatch];
+#pragma unroll
+    for (int u = 0; u < kScanBatch; ++u) {  // the next set bits, lowest first
+      live[u] = (m0 | m1) != 0;
+      if (m0) {
+        fs[u] = (uint32_t)__builtin_ctzll(m0);
+        m0 &= m0 - 1u;
+      } else if (m1) {
+        fs[u] = 64u + (uint32_t)__builtin_ctzll(m1);
+        m1 &= m1 - 1u;
+      } else {
+        fs[u] = u ? fs[u - 1] : 0u;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kScanBatch; ++u) {
+      const uint32_t j = rc.slot_skip(fs[u]);
+      q[u] = load(j);
+      qi[u] = kPads ? sl.idx_s[j] : j;
+    }
+#pragma unroll
+    for (int u = 0; u < kScanBatch; ++u)
+      if (live[u] && qi[u] != self) body(q[u]);
+  }
+}
+
+template <int kScanBatch, bool kPads, class Load, class Body>
+__device__ __forceinline__ void scan_runs(const SphSlots& sl, const RunTable& runs, uint32_t f0,
+                                          uint32_t total, f2 p, float r2, uint32_t self, Load&& load,
+                                          Body&& body) {
+  RunCursor rc(runs);
+  for (uint32_t f = f0; f < total; f += kScanBatch) {
+    f4 q[kScanBatch];
+    uint32_t qi[kScanBatch];
+#pragma unroll
+    for (int u = 0; u < kScanBatch; ++u) {
+      const uint32_t j = rc.slot_skip(min(f + u, total - 1u));
+      q[u] = load(j);
+      qi[u] = kPads ? sl.idx_s[j] : j;
+    }
+#pragma unroll
+    for (int u = 0; u < kScanBatch; ++u) {
+      if (f + u < total && qi[u] != self) {
+        const float dx = q[u][0] - p[0], dy = q[u][1] - p[1];
+        if (!(dx * dx + dy * dy > r2)) body(q[u]);
+      }
+    }
+  }
+}
+
 // simulation_step, compute_shader.wgsl:435-453: pressure (:256-334) and viscosity
 // (:336-384) against the start-of-pass velocity snapshot (rec_pv.zw), Euler (:392-395) and
 // walls (:69-99).  The new packed state of particle i goes to st2[i].
-// Self-skip (wgsl:295, :365) compares particle indices.  With P == N there are no pad entries,
-// every particle owns exactly one slot, and the index test is the slot test j != t: that
-// saves the 4-B index load per scanned entry (kPads = false).
 template <int kScanBatch, bool kPads>
 __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __restrict__ cfg,
                                                          const uint32_t* __restrict__ offsets,
@@ -929,80 +1011,58 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
   __shared__ RunTable runs;
   const uint32_t total = nine_runs(offsets, ends, p[0], p[1], cfg->screen_bounds[1],
                                    cfg->screen_bounds[3], r, N, runs);
+  const bool masked = total <= 128u;
+  const uint64_t m0 = masked ? sl.nbr_mask[t] : 0u, m1 = masked ? sl.nbr_mask[p_slots + t] : 0u;
   float fx = 0.0f, fy = 0.0f;
-  RunCursor rc(runs);
-  for (uint32_t f = 0; f < total; f += kScanBatch) {
-    f4 q[kScanBatch];
-    uint32_t qi[kScanBatch];
-#pragma unroll
-    for (int u = 0; u < kScanBatch; ++u) {
-      const uint32_t j = rc.slot(min(f + u, total - 1u));
-      q[u] = sl.rec_pd[j];
-      qi[u] = kPads ? sl.idx_s[j] : j;
+  const auto load_pd = [&](uint32_t j) { return sl.rec_pd[j]; };
+  const auto pressure = [&](const f4& q) {
+    const float dx = q[0] - p[0], dy = q[1] - p[1];
+    const float dist = sqrtf(dx * dx + dy * dy);
+    float dirx, diry;
+    if (dist > 0.0001f) {
+      dirx = dx / dist;
+      diry = dy / dist;
+    } else {
+      dirx = 0.0f;
+      diry = 1.0f;
     }
-#pragma unroll
-    for (int u = 0; u < kScanBatch; ++u) {
-      if (f + u < total && qi[u] != self) {
-        const float dx = q[u][0] - p[0], dy = q[u][1] - p[1];
-        const float sq = dx * dx + dy * dy;
-        if (!(sq > r2)) {
-          const float dist = sqrtf(sq);
-          float dirx, diry;
-          if (dist > 0.0001f) {
-            dirx = dx / dist;
-            diry = dy / dist;
-          } else {
-            dirx = 0.0f;
-            diry = 1.0f;
-          }
-          const float pt = P_rho2 + q[u][2];    // + Pj / (rj * rj)
-          const float npt = Pn_rho2 + q[u][3];  // + Pnj / (rj * rnj)
-          float dk = 0.0f, ndk = 0.0f;
-          if (!(dist >= r)) {
-            const float v = r - dist;
-            dk = (-2.0f * dn) * v;
-            ndk = ((-3.0f * ndn) * v) * v;
-          }
-          fx = fx + (dirx * pt) * dk;
-          fy = fy + (diry * pt) * dk;
-          fx = fx + (dirx * npt) * ndk;
-          fy = fy + (diry * npt) * ndk;
-        }
-      }
+    const float pt = P_rho2 + q[2];    // + Pj / (rj * rj)
+    const float npt = Pn_rho2 + q[3];  // + Pnj / (rj * rnj)
+    float dk = 0.0f, ndk = 0.0f;
+    if (!(dist >= r)) {
+      const float v = r - dist;
+      dk = (-2.0f * dn) * v;
+      ndk = ((-3.0f * ndn) * v) * v;
     }
-  }
+    fx = fx + (dirx * pt) * dk;
+    fy = fy + (diry * pt) * dk;
+    fx = fx + (dirx * npt) * ndk;
+    fy = fy + (diry * npt) * ndk;
+  };
+  if (masked)
+    scan_masked<kScanBatch, kPads>(sl, runs, m0, m1, self, load_pd, pressure);
+  else
+    scan_runs<kScanBatch, kPads>(sl, runs, 0u, total, p, r2, self, load_pd, pressure);
   const f4 own_pv = sl.rec_pv[t];
   float qx = own_pv[2] + fx * dt;  // post-gravity velocity (the pre pass, wgsl:397-400)
   float qy = own_pv[3] + fy * dt;
   float wx = 0.0f, wy = 0.0f;
-  RunCursor rc2(runs);
-  for (uint32_t f = 0; f < total; f += kScanBatch) {
-    f4 q[kScanBatch];
-    uint32_t qi[kScanBatch];
-#pragma unroll
-    for (int u = 0; u < kScanBatch; ++u) {
-      const uint32_t j = rc2.slot(min(f + u, total - 1u));
-      q[u] = sl.rec_pv[j];
-      qi[u] = kPads ? sl.idx_s[j] : j;
+  const auto load_pv = [&](uint32_t j) { return sl.rec_pv[j]; };
+  const auto viscosity = [&](const f4& q) {
+    const float dx = p[0] - q[0], dy = p[1] - q[1];
+    const float dist = sqrtf(dx * dx + dy * dy);
+    float k = 0.0f;
+    if (!(dist >= r)) {
+      const float v = r * r - dist * dist;
+      k = ((vn * v) * v) * v;
     }
-#pragma unroll
-    for (int u = 0; u < kScanBatch; ++u) {
-      if (f + u < total && qi[u] != self) {
-        const float dx = p[0] - q[u][0], dy = p[1] - q[u][1];
-        const float sq = dx * dx + dy * dy;
-        if (!(sq > r2)) {
-          const float dist = sqrtf(sq);
-          float k = 0.0f;
-          if (!(dist >= r)) {
-            const float v = r * r - dist * dist;
-            k = ((vn * v) * v) * v;
-          }
-          wx = wx + (q[u][2] - qx) * k;
-          wy = wy + (q[u][3] - qy) * k;
-        }
-      }
-    }
-  }
+    wx = wx + (q[2] - qx) * k;
+    wy = wy + (q[3] - qy) * k;
+  };
+  if (masked)
+    scan_masked<kScanBatch, kPads>(sl, runs, m0, m1, self, load_pv, viscosity);
+  else
+    scan_runs<kScanBatch, kPads>(sl, runs, 0u, total, p, r2, self, load_pv, viscosity);
   qx = qx + (wx * cfg->viscocity_strength) * dt;
   qy = qy + (wy * cfg->viscocity_strength) * dt;
   const f2 c = sl.cur_s[t];
