@@ -239,7 +239,9 @@ int rps_step(rps_ctx* ctx, uint32_t nsteps);
 int rps_update(rps_ctx* ctx);
 int rps_sync(rps_ctx* ctx);
 
-/* Stats of the most recent reduced step (requires RPS_EXT_STATS); blocks. */
+/* Stats of the most recent reduced step (requires RPS_EXT_STATS); blocks.  With a
+ * communicator (rps_comm_init, STREAM mode) they cover every rank's shard: each stats step
+ * all-reduces bbox min/max and the KE / particle / respawn sums over the ranks (RCCL). */
 int rps_get_stats(rps_ctx* ctx, rps_stats* out);
 
 /* Host-visible counters: frame_count of the device config and active steps executed. */
@@ -262,7 +264,8 @@ void* rps_get_stream(rps_ctx* ctx);
  * mode/config; `unit` receives 0 for bytes, 1 for flops. */
 int rps_step_cost(const rps_ctx* ctx, double* amount, int* unit);
 
-/* Multi-GPU (N-body mode only needs it): RCCL communicator over this rank's context.
+/* Multi-GPU: RCCL communicator over this rank's context.  N-body needs it (all-gather of
+ * positions); STREAM uses it only for the all-rank stats (rps_get_stats).
  * unique_id is the 128-byte ncclUniqueId produced by rps_comm_unique_id on rank 0. */
 int rps_comm_unique_id(void* out128);
 /* N-body sources: the device array of float2 positions of ALL global particles (global_count

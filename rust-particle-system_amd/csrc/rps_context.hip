@@ -65,6 +65,7 @@ struct rps_ctx {
   StatsPartial* partials = nullptr;
   uint32_t partial_cap = 0;
   StatsResult* d_stats = nullptr;
+  StatsGlobal* d_gstats = nullptr;  // all-rank stats (with a communicator)
   bool have_stats = false;
   // staging for AoS transfers
   rps_particle* d_staging = nullptr;
@@ -275,6 +276,20 @@ SphBuffers sph_buffers(rps_ctx* ctx) {
   return b;
 }
 
+// Sharded STREAM runs with a communicator: the stats of a stats step over all ranks, two
+// in-place all-reduces of 16 + 24 bytes on the context stream (MAX of the bbox terms, SUM of
+// KE and counts), amortised over stats_interval steps.
+int allreduce_stats(rps_ctx* ctx) {
+  if (!ctx->comm) return RPS_OK;
+  ncclResult_t r = ncclAllReduce(ctx->d_gstats->neg_min_max, ctx->d_gstats->neg_min_max, 4, ncclFloat,
+                                 ncclMax, ctx->comm, ctx->stream);
+  if (r == ncclSuccess)
+    r = ncclAllReduce(ctx->d_gstats->sums, ctx->d_gstats->sums, 3, ncclDouble, ncclSum, ctx->comm,
+                      ctx->stream);
+  if (r != ncclSuccess) return fail(ctx, RPS_ERR_COMM, std::string("ncclAllReduce(stats): ") + ncclGetErrorString(r));
+  return RPS_OK;
+}
+
 int step_stream(rps_ctx* ctx) {
   const uint64_t k = ctx->active_steps;
   const rps_ext_config& e = ctx->ext;
@@ -301,7 +316,9 @@ int step_stream(rps_ctx* ctx) {
   if (rc) return rc;
   if (stats) {
     RPS_HIP(ctx, launch_stats_finalize(ctx->partials, l.grid, ctx->partials + ctx->partial_cap,
-                                       ctx->d_stats, k, ctx->stream));
+                                       ctx->d_stats, ctx->comm ? ctx->d_gstats : nullptr, k, ctx->stream));
+    rc = allreduce_stats(ctx);
+    if (rc) return rc;
     ctx->have_stats = true;
   }
   return RPS_OK;
@@ -344,7 +361,10 @@ int step_stream_fused(rps_ctx* ctx, uint64_t k0, uint32_t m, bool stats, uint64_
   if (rc) return rc;
   if (stats) {
     RPS_HIP(ctx, launch_stats_finalize(ctx->partials, l.grid, ctx->partials + ctx->partial_cap,
-                                       ctx->d_stats, k0 + m - 1, ctx->stream));
+                                       ctx->d_stats, ctx->comm ? ctx->d_gstats : nullptr, k0 + m - 1,
+                                       ctx->stream));
+    rc = allreduce_stats(ctx);
+    if (rc) return rc;
     ctx->have_stats = true;
   }
   return RPS_OK;
@@ -539,6 +559,7 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
   }
   slots.push_back({(void**)&ctx->d_cfg, align_up(sizeof(rps_config), 256)});
   slots.push_back({(void**)&ctx->d_stats, align_up(sizeof(StatsResult), 256)});
+  slots.push_back({(void**)&ctx->d_gstats, align_up(sizeof(StatsGlobal), 256)});
   std::vector<size_t> offs;
   for (auto& s : slots) {
     offs.push_back(off);
@@ -909,13 +930,24 @@ int rps_get_stats(rps_ctx* ctx, rps_stats* out) {
   if (!out) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "null output");
   if (!ctx->have_stats) return fail(ctx, RPS_ERR_UNSUPPORTED, "no stats reduced yet (RPS_EXT_STATS)");
   StatsResult r;
+  StatsGlobal g;
   RPS_HIP(ctx, hipMemcpyAsync(&r, ctx->d_stats, sizeof(r), hipMemcpyDeviceToHost, ctx->stream));
+  if (ctx->comm) RPS_HIP(ctx, hipMemcpyAsync(&g, ctx->d_gstats, sizeof(g), hipMemcpyDeviceToHost, ctx->stream));
   RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
   for (int k = 0; k < 4; ++k) out->bbox[k] = r.bbox[k];
   out->kinetic_energy = r.ke;
   out->particles = r.count;
   out->respawned = r.respawned;
   out->step = r.step;
+  if (ctx->comm) {  // every rank's shard (allreduce_stats)
+    out->bbox[0] = -g.neg_min_max[0];
+    out->bbox[1] = g.neg_min_max[1];
+    out->bbox[2] = -g.neg_min_max[2];
+    out->bbox[3] = g.neg_min_max[3];
+    out->kinetic_energy = g.sums[0];
+    out->particles = (uint64_t)g.sums[1];
+    out->respawned = (uint64_t)g.sums[2];
+  }
   return RPS_OK;
 }
 

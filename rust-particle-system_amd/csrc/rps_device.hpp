@@ -120,6 +120,14 @@ struct StatsResult {
   unsigned long long step;
 };
 
+// A shard's stats in the form two in-place ncclAllReduce calls combine over the ranks
+// (DESIGN.md §8): MAX over {-x_min, x_max, -y_min, y_max}, SUM over {KE, particles,
+// respawns} (counts are exact in f64 below 2^53).
+struct StatsGlobal {
+  float neg_min_max[4];
+  double sums[3];
+};
+
 // ---------------------------------------------------------------------------------------
 // Random123 Philox4x32-10 (build-defined respawn stream, keyed by (seed, global id, step)).
 // ---------------------------------------------------------------------------------------

@@ -25,9 +25,10 @@ hipError_t launch_stream_step(const StreamArgs& a, const StreamLaunch& l, hipStr
 hipError_t launch_stream_fused(const FusedArgs& a, const StreamLaunch& l, hipStream_t s);
 // Deterministic two-level reduction of per-workgroup partials (scratch: kStatsFold entries).
 constexpr uint32_t kStatsFold = 256;
+// `global` (nullable): also the shard's stats in the all-reduce form (StatsGlobal).
 hipError_t launch_stats_finalize(const StatsPartial* partials, uint32_t count,
-                                 StatsPartial* scratch, StatsResult* out, uint64_t step,
-                                 hipStream_t s);
+                                 StatsPartial* scratch, StatsResult* out, StatsGlobal* global,
+                                 uint64_t step, hipStream_t s);
 
 hipError_t launch_aos_to_soa(const rps_particle* aos, Fields f, Layout L, uint64_t offset,
                              uint64_t n, hipStream_t s);

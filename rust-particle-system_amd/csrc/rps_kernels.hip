@@ -290,6 +290,7 @@ __global__ __launch_bounds__(kBlock) void stats_fold_kernel(const StatsPartial* 
 
 __global__ __launch_bounds__(kBlock) void stats_finalize_kernel(const StatsPartial* partials,
                                                                 uint32_t count, StatsResult* out,
+                                                                StatsGlobal* global,
                                                                 unsigned long long step) {
   StatsAcc acc;
   acc.init();
@@ -314,6 +315,17 @@ __global__ __launch_bounds__(kBlock) void stats_finalize_kernel(const StatsParti
     r.respawned = res[0].respawned;
     r.step = step;
     *out = r;
+    if (global) {
+      StatsGlobal g;
+      g.neg_min_max[0] = -r.bbox[0];
+      g.neg_min_max[1] = r.bbox[1];
+      g.neg_min_max[2] = -r.bbox[2];
+      g.neg_min_max[3] = r.bbox[3];
+      g.sums[0] = r.ke;
+      g.sums[1] = (double)r.count;
+      g.sums[2] = (double)r.respawned;
+      *global = g;
+    }
   }
 }
 
@@ -1157,8 +1169,8 @@ hipError_t launch_stream_fused(const FusedArgs& a, const StreamLaunch& l, hipStr
 }
 
 hipError_t launch_stats_finalize(const StatsPartial* partials, uint32_t count,
-                                 StatsPartial* scratch, StatsResult* out, uint64_t step,
-                                 hipStream_t s) {
+                                 StatsPartial* scratch, StatsResult* out, StatsGlobal* global,
+                                 uint64_t step, hipStream_t s) {
   if (count > kStatsFold) {
     const uint32_t chunk = (count + kStatsFold - 1) / kStatsFold;
     const uint32_t blocks = (count + chunk - 1) / chunk;
@@ -1170,7 +1182,7 @@ hipError_t launch_stats_finalize(const StatsPartial* partials, uint32_t count,
     count = blocks;
   }
   hipLaunchKernelGGL(stats_finalize_kernel, dim3(1), dim3(kBlock), 0, s, partials, count, out,
-                     (unsigned long long)step);
+                     global, (unsigned long long)step);
   return hipGetLastError();
 }
 

@@ -361,3 +361,31 @@ def test_lifetime_views_clock_and_toggle(gpu, orc):
         st = ctx.download_field(rps.FIELD_LIFE_STEPS)
         ctx.upload_field(rps.FIELD_LIFE_STEPS, st)
         assert_bitwise(ctx.read_debug(rps.DEBUG_EXPIRY), ref["exp"], "steps round trip")
+
+
+def test_stats_allreduce_single_rank(gpu, orc):
+    """STREAM with a communicator: every stats step all-reduces the shard stats over the ranks
+    (RCCL MAX of the bbox terms, SUM of KE / particles / respawns).  With one rank the
+    all-rank stats must equal the shard's, through the same RCCL calls; the state is
+    untouched by them (bitwise == oracle)."""
+    rps = gpu
+    n = 300001
+    cfg = config_c1(rps, n)
+    ext = rps.headline_ext(stats=True)
+    ext.shader_delay = 0
+    ext.stats_interval = 2
+    soa = random_soa(n, list(cfg.screen_bounds), seed=43, life=(-0.02, 0.5))
+    ref = copy_soa(soa)
+    with _gpu_ctx(rps, n, cfg, ext, soa) as ctx:
+        ctx.comm_init(0, 1, rps.comm_unique_id())
+        ctx.step(3)  # stats steps 0 and 2
+        st = ctx.stats()
+        got = ctx.download_soa(life=True)
+    for k in range(3):
+        ost = orc.stream_step(cfg, ext, ref, k, stats=(k == 2))
+    for key in ("x", "y", "vx", "vy", "life"):
+        assert_bitwise(got[key], ref[key], key)
+    assert st.step == 2 and st.particles == n
+    assert st.respawned == ost.respawned
+    assert list(st.bbox) == list(ost.bbox)
+    assert abs(st.kinetic_energy - ost.kinetic_energy) <= 1e-9 * abs(ost.kinetic_energy)
