@@ -617,14 +617,16 @@ __device__ __forceinline__ void sort_group(T mem, uint32_t base, uint32_t r, uin
 }
 
 // Groups of a (K, flip) chunk in an array of `len` entries, group q -> (base, residue).
+// len, G and g are powers of two (a flip chunk has g >= 2), so the split is shifts and masks
+// rather than a runtime u32 division per group.
 __device__ __forceinline__ uint32_t sort_groups(uint32_t len, uint32_t G, uint32_t g, bool flip) {
-  return (len / (2u * G)) * (flip ? g / 2u : g);
+  return (len >> (__builtin_ctz(G) + 1)) << (__builtin_ctz(g) - (flip ? 1 : 0));
 }
 __device__ __forceinline__ void sort_group_at(uint32_t q, uint32_t G, uint32_t g, bool flip,
                                               uint32_t& base, uint32_t& r) {
-  const uint32_t per = flip ? g / 2u : g;
-  base = (q / per) * 2u * G;
-  r = q % per;
+  const uint32_t lp = __builtin_ctz(g) - (flip ? 1u : 0u);  // log2(groups per 2G block)
+  base = (q >> lp) << (__builtin_ctz(G) + 1);
+  r = q & ((1u << lp) - 1u);
 }
 
 // K global passes of one stage, one group per thread.
