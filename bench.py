@@ -27,6 +27,11 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 METRIC = "particle-updates/sec + achieved HBM GB/s, 10^8 particles, 1/2/4/8 MI355X"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# SURVEY.md §8(d) / BASELINE.md, C3: the algorithmic cost of a particle-step is 40 B (read and
+# write x, y, vx, vy and an f32 lifetime).  The kernel moves 34 of them (the lifetime is a u16
+# expiry read each step and written only on respawn): that figure is reported
+# beside it as `moved_*`, and `traffic` is what the PMC counters measured.
+ALGO_BYTES_PER_PARTICLE = 40.0
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
@@ -247,14 +252,16 @@ def main():
     elapsed = d.max(t1 - t0)
     kern_ms, launches = ctx.kernel_time()
     kern_ms = d.max(kern_ms)
-    bytes_per_launch, _ = ctx.step_cost()
+    moved_per_launch, _ = ctx.step_cost()  # bytes the kernel moves: 34 B per particle
+    algo_per_launch = ALGO_BYTES_PER_PARTICLE * n
     st = ctx.stats()
     ctx.close()
 
     updates = float(n) * d.world * args.steps
     value = updates / elapsed
-    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-    hbm_wall = bytes_per_launch * args.steps / elapsed / 1e9  # per GPU, wall clock incl. gaps
+    achieved = algo_per_launch / (kern_ms * 1e-3) / 1e9
+    moved_gbps = moved_per_launch / (kern_ms * 1e-3) / 1e9
+    hbm_wall = moved_per_launch * args.steps / elapsed / 1e9  # per GPU, wall clock incl. gaps
     traffic = pmc_traffic(wl)
     line = {
         "metric": METRIC,
@@ -271,12 +278,15 @@ def main():
         "data": "synthetic (seeded device scatter of src/main.rs:182-216; Philox respawn)",
         "config": {"workload": wl, "particles_per_gpu": n, "global_particles": n * d.world,
                    "attractors": 4, "drag": 0.1, "lifetime_s": [1.0, 5.0], "integrator": "euler",
-                   "bytes_per_particle_step": bytes_per_launch / n, "parallelism": f"index-shard x{d.world}"},
+                   "bytes_per_particle_step": moved_per_launch / n, "parallelism": f"index-shard x{d.world}"},
         "hbm_gbps_per_gpu": hbm_wall,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS,
                      "traffic": traffic, "kernel": "stream_step_kernel<euler,lifetime>",
-                     "avg_kernel_ms": kern_ms, "launches": launches},
+                     "avg_kernel_ms": kern_ms, "launches": launches,
+                     "algorithmic_bytes_per_launch": algo_per_launch,
+                     "moved_bytes_per_launch": moved_per_launch, "moved_gbps": moved_gbps,
+                     "moved_frac": moved_gbps / HBM_PEAK_GBPS},
         "stats": {"bbox": list(st.bbox), "respawned_last": st.respawned, "particles": st.particles},
     }
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
