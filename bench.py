@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--sph-n", type=int, default=1 << 22,
                     help="particles of the SPH-frame side measurement per rank (0: skip)")
     ap.add_argument("--sph-frames", type=int, default=50)
+    ap.add_argument("--sph-cpu-n", type=int, default=1 << 20,
+                    help="particles of the SPH CPU-baseline sample (oracle, one thread)")
+    ap.add_argument("--sph-cpu-frames", type=int, default=3)
     ap.add_argument("--allpairs-timeout", type=float, default=240.0,
                     help="watchdog: print the headline line and exit if the side run hangs")
     return ap.parse_args()
@@ -219,10 +222,36 @@ def sph_side(rps, args, d):
         sim_ms, _ = ctx.kernel_time()
     finally:
         ctx.close()
-    return {"workload": f"SPH frame (5 passes, bitwise == oracle), {n} particles per rank, reference scatter",
-            "scaling": "replicas", "frames": args.sph_frames, "ms_per_frame": el * 1e3 / args.sph_frames,
-            "particle_steps_per_s": float(n) * d.world * args.sph_frames / el,
-            "sim_kernel_ms": d.max(sim_ms)}
+    out = {"workload": f"SPH frame (5 passes, bitwise == oracle), {n} particles per rank, reference scatter",
+           "scaling": "replicas", "frames": args.sph_frames, "ms_per_frame": el * 1e3 / args.sph_frames,
+           "particle_steps_per_s": float(n) * d.world * args.sph_frames / el,
+           "sim_kernel_ms": d.max(sim_ms)}
+    if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline and args.sph_cpu_n > 0:
+        out["cpu_baseline"] = sph_cpu_baseline(rps, args)
+    return out
+
+
+def sph_cpu_baseline(rps, args):
+    """The reference's SPH frame on the host: the oracle's restatement of the five WGSL passes
+    (oracle/rps_oracle.c, one thread) over a bounded sample of the same workload (the
+    reference scatter at the default density), timed after one warm frame."""
+    import oracle as orc
+
+    n = args.sph_cpu_n
+    scale = max(1.0, (n / 50000) ** 0.5)
+    cfg = rps.default_particle_config(n, screen_bounds=rps.screen_bounds_for(1920.0 * scale, 1080.0 * scale))
+    parts = rps.setup_particles_scatter(cfg, n, seed=args.seed)
+    soa = dict(x=parts["position"][:, 0].copy(), y=parts["position"][:, 1].copy(),
+               vx=parts["velocity"][:, 0].copy(), vy=parts["velocity"][:, 1].copy())
+    st = orc.SphState(n)
+    ext = rps.make_ext(shader_delay=0)
+    fc, _ = orc.run_steps(2, cfg, ext, soa, 1, sph=st)  # warm frame
+    t0 = time.perf_counter()
+    orc.run_steps(2, cfg, ext, soa, args.sph_cpu_frames, frame_count=fc, sph=st)
+    el = time.perf_counter() - t0
+    return {"value": float(n) * args.sph_cpu_frames / el, "unit": "particle-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{n} particles x {args.sph_cpu_frames} frames of the five passes (oracle/rps_oracle.c, "
+                      f"one thread), {el:.1f} s; {el * 1e3 / args.sph_cpu_frames:.0f} ms/frame"}
 
 
 def main():
