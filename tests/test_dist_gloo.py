@@ -4,6 +4,9 @@
   the unsharded step bit for bit (no data-path collective needed).
 * NBODY: each rank all-gathers the float2 positions (the exchange rps_step does with
   ncclAllGather) and computes forces for its own targets == the unsharded forces.
+* STREAM stats over ranks: each shard's stats in the form librps all-reduces over RCCL
+  (StatsGlobal, rps_device.hpp: MAX of {-x_min, x_max, -y_min, y_max}, SUM of KE, particles,
+  respawns) combine to the unsharded stats.
 * bench.Dist: barrier + max-over-ranks as used by bench.py under torchrun.
 """
 import os
@@ -91,6 +94,36 @@ def _nbody_worker(rank, world, port, n_per, q):
     dist.destroy_process_group()
 
 
+def _stats_worker(rank, world, port, n_per, q):
+    _setup(rank, world, port)
+    import oracle as orc
+    import rps_amd as rps
+    from helpers import random_soa
+
+    cfg = rps.default_particle_config(n_per * world)
+    ext = rps.headline_ext(stats=True)
+    full = random_soa(n_per * world, list(cfg.screen_bounds), seed=91, life=(-0.1, 0.5))
+    lo = rank * n_per
+    mine = {k: v[lo:lo + n_per].copy() for k, v in full.items()}
+    for s in range(4):
+        st = orc.stream_step(cfg, ext, mine, s, id_offset=lo, stats=(s == 3))
+    mm = torch.tensor([-st.bbox[0], st.bbox[1], -st.bbox[2], st.bbox[3]], dtype=torch.float32)
+    sums = torch.tensor([st.kinetic_energy, float(st.particles), float(st.respawned)], dtype=torch.float64)
+    dist.all_reduce(mm, op=dist.ReduceOp.MAX)  # == the two in-place ncclAllReduce calls
+    dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+    if rank == 0:
+        ref = {k: v.copy() for k, v in full.items()}
+        for s in range(4):
+            rst = orc.stream_step(cfg, ext, ref, s, stats=(s == 3))
+        bbox = np.array([-mm[0].item(), mm[1].item(), -mm[2].item(), mm[3].item()], np.float32)
+        ok = (np.array_equal(bbox, np.array(list(rst.bbox), np.float32)) and int(sums[1].item()) == rst.particles
+              and int(sums[2].item()) == rst.respawned and rst.respawned > 0
+              and abs(sums[0].item() - rst.kinetic_energy) <= 1e-9 * abs(rst.kinetic_energy))
+        q.put(int(ok))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def _bench_dist_worker(rank, world, port, q):
     for p in (ROOT,):
         if p not in sys.path:
@@ -121,6 +154,10 @@ def test_stream_shards_equal_unsharded_gloo():
 
 def test_nbody_allgather_shards_equal_unsharded_gloo():
     assert _run(_nbody_worker, 700) == 1
+
+
+def test_stream_stats_allreduce_form_gloo():
+    assert _run(_stats_worker, 5003) == 1
 
 
 def test_bench_dist_barrier_and_max_gloo():
