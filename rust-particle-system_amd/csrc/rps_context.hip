@@ -40,6 +40,7 @@ struct rps_ctx {
   float* state = nullptr;          // STREAM: the tiled x|y|vx|vy|expiry block
   float *x = nullptr, *y = nullptr, *vx = nullptr, *vy = nullptr;
   uint16_t* exp = nullptr;         // STREAM: lifetime expiry (u16)
+  uint16_t* next = nullptr;        // STREAM: per-quad earliest expiry (rps_device.hpp)
   // SPH: packed {x, y, vx, vy} state (x..vy point into st, layout sph_layout())
   f4* st = nullptr;
   f4* st2 = nullptr;       // sim-pass output, swapped with st after the pass
@@ -183,6 +184,7 @@ StreamArgs make_stream_args(const rps_ctx* ctx, uint64_t k) {
   a.vx = ctx->vx;
   a.vy = ctx->vy;
   a.exp = ctx->exp;
+  a.next = ctx->next;
   a.clock = (uint32_t)ctx->life_clock;
   a.partials = ctx->partials;
   a.n = ctx->n;
@@ -521,7 +523,7 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
   struct Slot { void** p; size_t bytes; };
   std::vector<Slot> slots;
   if (ctx->mode == RPS_MODE_STREAM) {
-    // Tiled SoA: ceil(n / kTile) tiles of 4 f32 + 1 u16 segments (rps_device.hpp).
+    // Tiled SoA: ceil(n / kTile) tiles of 4 f32 + 2 u16 segments (rps_device.hpp).
     const size_t tiles = (n + kTile - 1) / kTile;
     slots.push_back({(void**)&ctx->state, tiles * kTileBytes});
   } else if (ctx->mode == RPS_MODE_NBODY) {
@@ -583,6 +585,7 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     ctx->vx = ctx->state + 2 * kTile;
     ctx->vy = ctx->state + 3 * kTile;
     ctx->exp = reinterpret_cast<uint16_t*>(ctx->state + 4 * kTile);
+    ctx->next = ctx->exp + kTile;  // zero-filled with the arena: expiries 0, clock 0, next 0
     ctx->exp_layout = tiled_exp_layout();
   }
   // wgpu buffers are zero-initialised; the SPH lookup pad entries rely on it.
@@ -752,9 +755,13 @@ int rps_upload_field(rps_ctx* ctx, int field, const float* src, uint64_t offset,
     const uint64_t m = std::min(chunk, n - done);
     RPS_HIP(ctx, hipMemcpyAsync(stage, src + done, m * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
     if (life)
+    {
       RPS_HIP(ctx, launch_life_scatter(ctx->exp, ctx->exp_layout, offset + done, stage, m,
                                        (uint32_t)ctx->life_clock, ctx->cfg.fixed_delta_time,
                                        field == RPS_FIELD_LIFE ? 0 : 2, ctx->stream));
+      RPS_HIP(ctx, launch_next_rebuild(ctx->exp, ctx->next, offset + done, m, ctx->n,
+                                       (uint32_t)ctx->life_clock, ctx->stream));
+    }
     else
       RPS_HIP(ctx, launch_field_scatter(p, ctx->layout, offset + done, stage, m, ctx->stream));
     RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -857,6 +864,9 @@ int rps_init_scatter(rps_ctx* ctx, uint64_t seed) {
   a.key0 = (uint32_t)seed;
   a.key1 = (uint32_t)(seed >> 32);
   RPS_HIP(ctx, launch_init_scatter(a, ctx->stream));
+  if (ctx->next)
+    RPS_HIP(ctx, launch_next_rebuild(ctx->exp, ctx->next, 0, ctx->n, ctx->n, (uint32_t)ctx->life_clock,
+                                     ctx->stream));
   return RPS_OK;
 }
 
@@ -1010,8 +1020,9 @@ int rps_step_cost(const rps_ctx* ctx, double* amount, int* unit) {
   if (!ctx || !amount || !unit) return fail(nullptr, RPS_ERR_INVALID_ARGUMENT, "null argument");
   switch (ctx->mode) {
     case RPS_MODE_STREAM: {
-      // r+w of x, y, vx, vy (+ the u16 expiry read): DESIGN.md §5.
-      const double per = (ctx->ext.flags & RPS_EXT_LIFETIME) ? 34.0 : 32.0;
+      // r+w of x, y, vx, vy (+ the quad's u16 [next] read, 0.5 B per particle; the expiries of
+      // the few quads with one due are read and written on top): DESIGN.md §5.
+      const double per = (ctx->ext.flags & RPS_EXT_LIFETIME) ? 32.5 : 32.0;
       *amount = per * (double)ctx->n;
       *unit = 0;
       return RPS_OK;

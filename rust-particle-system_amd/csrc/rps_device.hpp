@@ -19,18 +19,19 @@ constexpr int kMaxAttractors = 8;
 
 // Particle-state layout in HBM.  STREAM mode keeps the state as *tiled SoA*
 // (AoSoA): tiles of kTile particles, each tile holding four contiguous f32 segments
-// [x | y | vx | vy] followed by one u16 segment [expiry] (kTile * 18 B = 144 KiB).  Lanes
-// read 16 contiguous bytes (8 for the expiry) and a wave 1 KiB of one field, and a
-// workgroup's streams fall in one 144 KiB region instead of arrays gigabytes apart
-// (tools/hbm_probe.hip: 6.35-6.39 TB/s tiled vs 5.3 TB/s plain SoA on the in-place update).
-// SPH and N-body keep plain SoA.
+// [x | y | vx | vy], one u16 segment [expiry] and one u16 segment [next] with an entry per
+// quad of 4 particles: the quad's earliest expiry, so a step reads the four expiries only in
+// the quad-steps where one of them is due (kTile * 18.5 B = 148 KiB per tile).  Lanes read
+// 16 contiguous bytes of each f32 field and 2 of [next]; a workgroup's streams fall in one
+// tile instead of arrays gigabytes apart (tools/hbm_probe.hip: 6.35-6.39 TB/s tiled vs
+// 5.3 TB/s plain SoA on the in-place update).  SPH and N-body keep plain SoA.
 constexpr uint32_t kTileLog = 13;
 constexpr uint64_t kTile = 1ull << kTileLog;
-constexpr uint64_t kTileBytes = kTile * 18;  // 4 x f32 + 1 x u16 per particle
+constexpr uint64_t kTileBytes = kTile * 37 / 2;  // 4 x f32 + 1 x u16 per particle + u16 per quad
 
 // Element offset of particle i inside one field: (((i & ~mask) * mult) >> shift) + (i & mask).
-// plain: mask = ~0 (offset i).  Tiled f32 fields: the tile stride is 4.5 * kTile floats
-// (mult 9, shift 1); the tiled u16 expiry: 9 * kTile u16 (mult 9, shift 0).
+// plain: mask = ~0 (offset i).  Tiled f32 fields: the tile stride is 4.625 * kTile floats
+// (mult 37, shift 3); the tiled u16 expiry: 9.25 * kTile u16 (mult 37, shift 2).
 struct Layout {
   uint64_t mask;
   uint64_t mult;
@@ -40,14 +41,28 @@ __host__ __device__ __forceinline__ uint64_t lidx(Layout L, uint64_t i) {
   return (((i & ~L.mask) * L.mult) >> L.shift) + (i & L.mask);
 }
 __host__ __device__ __forceinline__ Layout plain_layout() { return Layout{~0ull, 1, 0}; }
-__host__ __device__ __forceinline__ Layout tiled_layout() { return Layout{kTile - 1, 9, 1}; }
-__host__ __device__ __forceinline__ Layout tiled_exp_layout() { return Layout{kTile - 1, 9, 0}; }
+__host__ __device__ __forceinline__ Layout tiled_layout() { return Layout{kTile - 1, 37, 3}; }
+__host__ __device__ __forceinline__ Layout tiled_exp_layout() { return Layout{kTile - 1, 37, 2}; }
 // Tiled offsets with compile-time constants (the stream kernel's address math).
 __device__ __forceinline__ uint64_t tidx(uint64_t i) {
-  return (((i & ~(kTile - 1)) * 9) >> 1) + (i & (kTile - 1));
+  return (((i & ~(kTile - 1)) * 37) >> 3) + (i & (kTile - 1));
 }
 __device__ __forceinline__ uint64_t eidx(uint64_t i) {
-  return (i & ~(kTile - 1)) * 9 + (i & (kTile - 1));
+  return (((i & ~(kTile - 1)) * 37) >> 2) + (i & (kTile - 1));
+}
+// [next] entry of the quad holding particle i (from the [next] segment of tile 0).
+__host__ __device__ __forceinline__ uint64_t nidx(uint64_t i) {
+  return (((i & ~(kTile - 1)) * 37) >> 2) + ((i & (kTile - 1)) >> 2);
+}
+// Earliest expiry of a quad as seen at lifetime clock c: the expiry e with the smallest
+// (u16)(e - c), i.e. the next step in which one of the four respawns.
+__host__ __device__ __forceinline__ uint16_t quad_next(uint16_t e0, uint16_t e1, uint16_t e2,
+                                                       uint16_t e3, uint16_t c) {
+  uint16_t best = e0;
+  if ((uint16_t)(e1 - c) < (uint16_t)(best - c)) best = e1;
+  if ((uint16_t)(e2 - c) < (uint16_t)(best - c)) best = e2;
+  if ((uint16_t)(e3 - c) < (uint16_t)(best - c)) best = e3;
+  return best;
 }
 
 // Base pointers of the fields; for the tiled layout f32 field f starts at tile-0 offset
@@ -77,7 +92,8 @@ struct StreamArgs {
   float* __restrict__ y;
   float* __restrict__ vx;
   float* __restrict__ vy;
-  uint16_t* __restrict__ exp;  // lifetime expiry, tiled u16 (eidx)
+  uint16_t* __restrict__ exp;   // lifetime expiry, tiled u16 (eidx)
+  uint16_t* __restrict__ next;  // per quad: its earliest expiry (nidx, quad_next)
   struct StatsPartial* partials;  // one per workgroup when stats are on
   uint64_t n;                     // particles in this shard
   uint64_t id_offset;             // global id of particle 0

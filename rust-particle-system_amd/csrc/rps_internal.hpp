@@ -45,6 +45,11 @@ hipError_t launch_life_gather(const uint16_t* exp, Layout L, uint64_t offset, fl
 hipError_t launch_life_scatter(uint16_t* exp, Layout L, uint64_t offset, const float* in,
                                uint64_t n, uint32_t clock, float dt, int mode, hipStream_t s);
 
+// Per-quad earliest expiries ([next], rps_device.hpp) of the full quads overlapping particles
+// [first, first + n) of a shard of `total`, from the expiries at lifetime clock `clock`.
+hipError_t launch_next_rebuild(const uint16_t* exp, uint16_t* next, uint64_t first, uint64_t n,
+                               uint64_t total, uint32_t clock, hipStream_t s);
+
 struct InitArgs {
   Fields f;  // exp may be null
   Layout layout, exp_layout;

@@ -234,7 +234,7 @@ def test_profiling_counts_dominant_kernel(gpu):
         ms, cnt = ctx.kernel_time()
         assert cnt == 7 and ms > 0
         amt, unit = ctx.step_cost()
-        assert unit == "bytes" and amt == 34.0 * n
+        assert unit == "bytes" and amt == 32.5 * n  # x, y, vx, vy r+w + the quads' [next] read
         assert ctx.time_steps(3) > 0
 
 
@@ -389,3 +389,37 @@ def test_stats_allreduce_single_rank(gpu, orc):
     assert st.respawned == ost.respawned
     assert list(st.bbox) == list(ost.bbox)
     assert abs(st.kinetic_energy - ost.kinetic_energy) <= 1e-9 * abs(ost.kinetic_energy)
+
+
+def test_quad_next_index_after_partial_lifetime_upload(gpu, orc):
+    """The per-quad earliest-expiry index ([next], rps_device.hpp) lets a step skip the
+    expiries of quads with none due.  It is rebuilt after every expiry write outside the
+    kernel: here a LIFE_STEPS upload over a range that starts and ends inside quads, with
+    lifetimes of 1-3 steps, then plain and temporally fused steps; every field and the raw
+    expiries stay bitwise equal to the oracle (which has no such index)."""
+    rps = gpu
+    n = 70003
+    cfg = config_c1(rps, n)
+    ext = rps.headline_ext()
+    ext.shader_delay = 0
+    soa = random_soa(n, list(cfg.screen_bounds), seed=57, life=(0.5, 3.0))
+    g = np.random.default_rng(58)
+    lo, m = 1001, 30001  # [1001, 31002): partial quads at both ends
+    steps = g.integers(1, 4, m).astype(F)
+    with _gpu_ctx(rps, n, cfg, ext, soa) as ctx:
+        ctx.step(2)
+        ctx.upload_field(rps.FIELD_LIFE_STEPS, steps, offset=lo)
+        ref = ctx.download_soa(life=True)
+        ref["exp"] = ctx.read_debug(rps.DEBUG_EXPIRY)
+        for k in range(2, 6):
+            orc.stream_step(cfg, ext, ref, k)
+        ctx.step(4)
+        assert_bitwise(ctx.read_debug(rps.DEBUG_EXPIRY), ref["exp"], "expiry after plain steps")
+        ext.fuse_steps = 3
+        ctx.set_config(cfg, ext)
+        for k in range(6, 13):
+            orc.stream_step(cfg, ext, ref, k)
+        ctx.step(7)
+        got = ctx.download_soa(life=True)
+        assert_soa_bitwise(got, ref, keys=KEYS5, what="fused ")
+        assert_bitwise(ctx.read_debug(rps.DEBUG_EXPIRY), ref["exp"], "expiry after fused steps")
