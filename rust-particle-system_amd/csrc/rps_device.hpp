@@ -319,17 +319,13 @@ __device__ __forceinline__ uint32_t respawn(const StreamArgs& a, uint64_t step, 
 }
 
 // Two particles, one active step (the kernels' unit: every op on the pair is one v_pk_*
-// where the ISA has it).  gid: global id of element 0 (element 1 is gid + 1).  Writes
-// re[i] = element i respawned.  With `single`, element 1 duplicates element 0 and only
-// element 0's lifetime is advanced (n % 4 tails).
-// att: this step's attractors; step: its active-step index (Philox counter); clock: its
-// lifetime-clock value; e[i]: expiries (the clock value of the step in which each
-// particle respawns, mod 2^16).
-template <bool VERLET, bool LIFETIME>
-__device__ __forceinline__ void step_pair(const StreamArgs& a, att_ptr att,
-                                          uint64_t step, uint32_t clock, uint64_t gid, f2& x,
-                                          f2& y, f2& vx, f2& vy, uint16_t e[2], bool re[2],
-                                          bool single = false) {
+// where the ISA has it), in two parts: step_pair_motion (forces, integration, walls) and
+// step_pair_life (lifetime expiry and respawn, after the walls).  The kernels run the motion
+// of all their pairs before the lifetime part, so a quad's expiries -- loaded only when one
+// is due -- are needed last and their load overlaps the motion arithmetic.
+template <bool VERLET>
+__device__ __forceinline__ void step_pair_motion(const StreamArgs& a, att_ptr att, f2& x, f2& y,
+                                                 f2& vx, f2& vy) {
   const float dt = a.dt;
   if constexpr (!VERLET) {
     vx = vx + a.gx_dt;  // apply_gravity, wgsl:397-400
@@ -367,17 +363,36 @@ __device__ __forceinline__ void step_pair(const StreamArgs& a, att_ptr att,
   for (int i = 0; i < 2; ++i) {
     float px = x[i], py = y[i], qx = vx[i], qy = vy[i];
     wall(a.x_min, a.x_max, a.y_min, a.y_max, a.damping, px, py, qx, qy);
-    re[i] = false;
-    if constexpr (LIFETIME) {
-      if ((i == 0 || !single) && e[i] == (uint16_t)clock) {
-        e[i] = (uint16_t)(clock + respawn(a, step, gid + i, px, py, qx, qy));
-        re[i] = true;
-      }
-    }
     x[i] = px;
     y[i] = py;
     vx[i] = qx;
     vy[i] = qy;
+  }
+}
+
+// The lifetime part of the step for two particles.  gid: global id of element 0 (element 1
+// is gid + 1); step: the active-step index (Philox counter); clock: the step's lifetime-clock
+// value; e[i]: expiries (the clock value of the step in which each particle respawns, mod
+// 2^16).  Writes re[i] = element i respawned.  With `single`, element 1 duplicates element 0
+// and only element 0's lifetime is advanced (n % 4 tails).
+template <bool LIFETIME>
+__device__ __forceinline__ void step_pair_life(const StreamArgs& a, uint64_t step, uint32_t clock,
+                                               uint64_t gid, f2& x, f2& y, f2& vx, f2& vy,
+                                               uint16_t e[2], bool re[2], bool single = false) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    re[i] = false;
+    if constexpr (LIFETIME) {
+      if ((i == 0 || !single) && e[i] == (uint16_t)clock) {
+        float px, py, qx, qy;
+        e[i] = (uint16_t)(clock + respawn(a, step, gid + i, px, py, qx, qy));
+        x[i] = px;
+        y[i] = py;
+        vx[i] = qx;
+        vy[i] = qy;
+        re[i] = true;
+      }
+    }
   }
 }
 

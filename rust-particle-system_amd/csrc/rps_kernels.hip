@@ -160,36 +160,56 @@ __device__ __forceinline__ att_ptr kernarg_f4(size_t offset) {
   return (att_ptr)((kchar)__builtin_amdgcn_kernarg_segment_ptr() + offset);
 }
 
-// Four particles of one lane (two f2 pairs) through `nsub` steps in registers.
+// Four particles of one lane (two f2 pairs) through `nsub` steps in registers: per step the
+// motion of both pairs, then their lifetimes (step_pair_motion / step_pair_life).
+// Eq: the quad's expiries as loaded (meaningful only if `due`); E receives the final ones.
 template <bool VERLET, bool LIFETIME>
 __device__ __forceinline__ void step_quad(const StreamArgs& a, att_ptr att0, size_t att_stride,
                                           uint32_t nsub, uint64_t step0, uint32_t clock0,
-                                          uint64_t gid, f4& X, f4& Y, f4& VX, f4& VY, h4& E,
-                                          bool re[4], bool& any) {
+                                          uint64_t gid, f4& X, f4& Y, f4& VX, f4& VY, h4 Eq,
+                                          bool due, uint16_t nx, h4& E, bool re[4], bool& any) {
+  f2 x[2] = {{X[0], X[1]}, {X[2], X[3]}}, y[2] = {{Y[0], Y[1]}, {Y[2], Y[3]}};
+  f2 vx[2] = {{VX[0], VX[1]}, {VX[2], VX[3]}}, vy[2] = {{VY[0], VY[1]}, {VY[2], VY[3]}};
+  bool r[4] = {false, false, false, false};
+  for (uint32_t sub = 0; sub < nsub; ++sub) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) step_pair_motion<VERLET>(a, att0 + sub * att_stride, x[p], y[p], vx[p], vy[p]);
+    if constexpr (LIFETIME) {
+      if (sub == 0) {
+        // First use of the expiry load, after the motion: the empty asm makes the load an
+        // unconditional instruction the compiler keeps in flight until here (a select on
+        // `due` at the load would be turned into a branch around it and force the wait
+        // before the motion).  Not due: no expiry equals any of the nsub clocks, so nx
+        // stands in for the quad's four (and is never written back).
+        asm volatile("" : "+v"(Eq));
+        E = due ? Eq : h4{nx, nx, nx, nx};
+      }
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        uint16_t e[2] = {E[2 * p], E[2 * p + 1]};
+        bool rr[2];
+        step_pair_life<LIFETIME>(a, step0 + sub, clock0 + sub, gid + 2 * p, x[p], y[p], vx[p], vy[p], e, rr);
+        E[2 * p] = e[0];
+        E[2 * p + 1] = e[1];
+        r[2 * p] |= rr[0];
+        r[2 * p + 1] |= rr[1];
+        any |= rr[0] | rr[1];
+      }
+    }
+  }
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
-    f2 x = {X[2 * p], X[2 * p + 1]}, y = {Y[2 * p], Y[2 * p + 1]};
-    f2 vx = {VX[2 * p], VX[2 * p + 1]}, vy = {VY[2 * p], VY[2 * p + 1]};
-    uint16_t e[2] = {E[2 * p], E[2 * p + 1]};
-    bool r[2] = {false, false};
-    for (uint32_t sub = 0; sub < nsub; ++sub) {
-      step_pair<VERLET, LIFETIME>(a, att0 + sub * att_stride, step0 + sub, clock0 + sub,
-                                  gid + 2 * p, x, y, vx, vy, e, r);
-      any |= r[0] | r[1];
-    }
-    X[2 * p] = x[0];
-    X[2 * p + 1] = x[1];
-    Y[2 * p] = y[0];
-    Y[2 * p + 1] = y[1];
-    VX[2 * p] = vx[0];
-    VX[2 * p + 1] = vx[1];
-    VY[2 * p] = vy[0];
-    VY[2 * p + 1] = vy[1];
-    E[2 * p] = e[0];
-    E[2 * p + 1] = e[1];
-    re[2 * p] = r[0];
-    re[2 * p + 1] = r[1];
+    X[2 * p] = x[p][0];
+    X[2 * p + 1] = x[p][1];
+    Y[2 * p] = y[p][0];
+    Y[2 * p + 1] = y[p][1];
+    VX[2 * p] = vx[p][0];
+    VX[2 * p + 1] = vx[p][1];
+    VY[2 * p] = vy[p][0];
+    VY[2 * p + 1] = vy[p][1];
   }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) re[c] = r[c];
 }
 
 // One particle (n % 4 tails) through `nsub` steps: the pair path with element 1 a copy.
@@ -200,18 +220,20 @@ __device__ __forceinline__ bool step_single(const StreamArgs& a, att_ptr att0, s
                                             float& qy, uint16_t& pe, bool& any) {
   f2 x = {px, px}, y = {py, py}, vx = {qx, qx}, vy = {qy, qy};
   uint16_t e[2] = {pe, pe};
-  bool r[2] = {false, false};
+  bool r0 = false;
   for (uint32_t sub = 0; sub < nsub; ++sub) {
-    step_pair<VERLET, LIFETIME>(a, att0 + sub * att_stride, step0 + sub, clock0 + sub, gid, x, y,
-                                vx, vy, e, r, true);
-    any |= r[0];
+    step_pair_motion<VERLET>(a, att0 + sub * att_stride, x, y, vx, vy);
+    bool rr[2];
+    step_pair_life<LIFETIME>(a, step0 + sub, clock0 + sub, gid, x, y, vx, vy, e, rr, true);
+    r0 |= rr[0];
+    any |= rr[0];
   }
   px = x[0];
   py = y[0];
   qx = vx[0];
   qy = vy[0];
   pe = e[0];
-  return r[0];
+  return r0;
 }
 
 // Shared body of the one-step and the temporally fused kernels.
@@ -236,18 +258,17 @@ __device__ __forceinline__ void stream_body(const StreamArgs& a, att_ptr att0, s
     f4 Y = ld4<NTL>(a.y + o);
     f4 VX = ld4<NTL>(a.vx + o);
     f4 VY = ld4<NTL>(a.vy + o);
-    h4 E = {0, 0, 0, 0};
+    h4 E = {0, 0, 0, 0}, Eq = {0, 0, 0, 0};
     bool due = false;  // one of the quad's expiries falls in this launch's steps
     if constexpr (LIFETIME) {
       due = (uint16_t)(nx - (uint16_t)a.clock) < nsub;
-      // Not due: no expiry equals any of the nsub clocks, so the quad's own expiries
-      // would compare unequal too; nx stands in for them (and is never written back).
-      if (due) E = lde4<NTL>(a.exp + eidx(i));
-      else E = h4{nx, nx, nx, nx};
+      // Every lane issues the expiry load; a lane with nothing due reads the first 8 B of the
+      // expiry segment instead (one cached line for the whole wave), so no bytes move for it.
+      Eq = *reinterpret_cast<const h4*>(a.exp + (due ? eidx(i) : 0));
     }
     bool re[4], any = false;
     step_quad<VERLET, LIFETIME>(a, att0, att_stride, nsub, step0, a.clock, a.id_offset + i, X, Y, VX,
-                                VY, E, re, any);
+                                VY, Eq, due, nx, E, re, any);
     if constexpr (STATS) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) acc.add(X[c], Y[c], VX[c], VY[c], re[c]);
