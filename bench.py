@@ -106,6 +106,15 @@ class Dist:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
+    def reduce(self, vals, op: str):
+        """Element-wise MAX or SUM of a list of floats over the ranks (f64)."""
+        if not self.dist:
+            return list(vals)
+        dev = f"cuda:{self.local}" if self.backend == "nccl" else "cpu"
+        t = self.torch.tensor(list(vals), dtype=self.torch.float64, device=dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX if op == "max" else self.dist.ReduceOp.SUM)
+        return [float(x) for x in t.cpu()]
+
     def close(self):
         if self.dist:
             self.dist.destroy_process_group()
@@ -116,6 +125,16 @@ def workload(rps, n_rank, world):
     ext = rps.headline_ext(stats=True)  # stats reduced every 100 steps (amortised)
     ext.shader_delay = 0  # every timed step is an active step
     return cfg, ext
+
+
+def global_stats(d, st):
+    """The last stats step over every rank's shard, combined after the timed region in the
+    form librps's own all-reduce uses (rps_get_stats with a communicator): MAX of the negated
+    minima and the maxima, SUM of KE, particles and respawns."""
+    mm = d.reduce([-st.bbox[0], st.bbox[1], -st.bbox[2], st.bbox[3]], "max")
+    ke, parts, resp = d.reduce([st.kinetic_energy, float(st.particles), float(st.respawned)], "sum")
+    return {"step": st.step, "bbox": [-mm[0], mm[1], -mm[2], mm[3]], "kinetic_energy": ke,
+            "respawned_last": int(resp), "particles": int(parts), "ranks": d.world}
 
 
 def pmc_traffic(workload_name):
@@ -317,7 +336,7 @@ def main():
                      "algorithmic_bytes_per_launch": algo_per_launch,
                      "moved_bytes_per_launch": moved_per_launch, "moved_gbps": moved_gbps,
                      "moved_frac": moved_gbps / HBM_PEAK_GBPS},
-        "stats": {"bbox": list(st.bbox), "respawned_last": st.respawned, "particles": st.particles},
+        "stats": global_stats(d, st),
     }
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(rps, args, cfg, ext)

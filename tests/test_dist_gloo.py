@@ -136,8 +136,17 @@ def _bench_dist_worker(rank, world, port, q):
     assert d.world == world and d.backend == "gloo"
     d.barrier()
     m = d.max(float(rank) + 0.5)
+
+    class St:  # one rank's last stats step (rps_stats)
+        bbox = [-10.0 - rank, 20.0 + rank, -30.0 + rank, 40.0 - rank]
+        kinetic_energy, particles, respawned, step = 1.5 * (rank + 1), 100 + rank, rank, 7
+
+    g = bench.global_stats(d, St())
+    ok = g == {"step": 7, "bbox": [-10.0 - (world - 1), 20.0 + world - 1, -30.0, 40.0], "ranks": world,
+               "kinetic_energy": 1.5 * world * (world + 1) / 2, "particles": 100 * world + world * (world - 1) // 2,
+               "respawned_last": world * (world - 1) // 2}
     if rank == 0:
-        q.put(m)
+        q.put(m if ok else -1.0)
     d.close()
 
 
