@@ -1020,9 +1020,9 @@ int rps_step_cost(const rps_ctx* ctx, double* amount, int* unit) {
   if (!ctx || !amount || !unit) return fail(nullptr, RPS_ERR_INVALID_ARGUMENT, "null argument");
   switch (ctx->mode) {
     case RPS_MODE_STREAM: {
-      // r+w of x, y, vx, vy (+ the quad's u16 [next] read, 0.5 B per particle; the expiries of
-      // the few quads with one due are read and written on top): DESIGN.md §5.
-      const double per = (ctx->ext.flags & RPS_EXT_LIFETIME) ? 32.5 : 32.0;
+      // r+w of x, y, vx, vy (+ the group's u16 [next] read, 2 B per 64 particles; the expiry
+      // lines of the groups with one due are read, and written on respawn, on top): DESIGN.md §5.
+      const double per = (ctx->ext.flags & RPS_EXT_LIFETIME) ? 32.0 + 2.0 / kGroup : 32.0;
       *amount = per * (double)ctx->n;
       *unit = 0;
       return RPS_OK;

@@ -20,9 +20,9 @@ constexpr int kMaxAttractors = 8;
 // Particle-state layout in HBM.  STREAM mode keeps the state as *tiled SoA*
 // (AoSoA): tiles of kTile particles, each tile holding four contiguous f32 segments
 // [x | y | vx | vy], one u16 segment [expiry] and one u16 segment [next] with an entry per
-// quad of 4 particles: the quad's earliest expiry, so a step reads the four expiries only in
-// the quad-steps where one of them is due (kTile * 18.5 B = 148 KiB per tile).  Lanes read
-// 16 contiguous bytes of each f32 field and 2 of [next]; a workgroup's streams fall in one
+// group of 64 particles: the group's earliest expiry, so a step reads the expiries only in
+// the group-steps where one of them is due (kTile * 18.5 B = 148 KiB per tile).  Lanes read
+// 16 contiguous bytes of each f32 field (16 lanes share a [next] entry); a workgroup's streams fall in one
 // tile instead of arrays gigabytes apart (tools/hbm_probe.hip: 6.35-6.39 TB/s tiled vs
 // 5.3 TB/s plain SoA on the in-place update).  SPH and N-body keep plain SoA.
 constexpr uint32_t kTileLog = 13;
@@ -50,9 +50,16 @@ __device__ __forceinline__ uint64_t tidx(uint64_t i) {
 __device__ __forceinline__ uint64_t eidx(uint64_t i) {
   return (((i & ~(kTile - 1)) * 37) >> 2) + (i & (kTile - 1));
 }
-// [next] entry of the quad holding particle i (from the [next] segment of tile 0).
+// [next] holds one entry per group of kGroup particles (16 quads: the 16 lanes of a DPP row),
+// so a step reads 2 B per 64 particles of it.  A group's expiries are 128 B, one cache line,
+// and the lines of due groups are the ones that move either way: per-quad entries (0.5 B per
+// particle) bought nothing over this but their own traffic.  The segment keeps kTile / 4
+// entries per tile; the first kTile / kGroup are used.
+constexpr uint32_t kGroupLog = 6;
+constexpr uint64_t kGroup = 1ull << kGroupLog;
+// [next] entry of the group holding particle i (from the [next] segment of tile 0).
 __host__ __device__ __forceinline__ uint64_t nidx(uint64_t i) {
-  return (((i & ~(kTile - 1)) * 37) >> 2) + ((i & (kTile - 1)) >> 2);
+  return (((i & ~(kTile - 1)) * 37) >> 2) + ((i & (kTile - 1)) >> kGroupLog);
 }
 // Earliest expiry of a quad as seen at lifetime clock c: the expiry e with the smallest
 // (u16)(e - c), i.e. the next step in which one of the four respawns.
@@ -155,10 +162,12 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t
       k0 += 0x9E3779B9u;
       k1 += 0xBB67AE85u;
     }
-    const uint32_t lo0 = 0xD2511F53u * c0;
-    const uint32_t hi0 = __umulhi(0xD2511F53u, c0);
-    const uint32_t lo1 = 0xCD9E8D57u * c2;
-    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2);
+    // One 32x32->64 product per word (v_mad_u64_u32: both halves from one quarter-rate op,
+    // where mul_lo + mul_hi take two).
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+    const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
     const uint32_t n0 = hi1 ^ c1 ^ k0;
     const uint32_t n2 = hi0 ^ c3 ^ k1;
     c0 = n0;

@@ -138,9 +138,10 @@ __device__ void block_reduce_stats(StatsAcc acc, StatsPartial* out) {
 // ---------------------------------------------------------------------------------------
 // Streaming step: one fused pass per active step.  SoA x|y|vx|vy read and written
 // in place with 16-B vector accesses (4 particles per lane), grid-stride.  32 B/particle
-// of x, y, vx, vy read+write; with lifetime +0.5 B: the quad's [next] (its earliest expiry),
-// and the quad's four expiries read (and written on respawn) only when one is due: 32.5 B per
-// particle plus ~1.3 % of quads' expiries at C3.
+// of x, y, vx, vy read+write; with lifetime +2 B per 64 particles: the group's [next] (its
+// earliest expiry), and the group's 64 expiries (one 128-B line) read, and written on
+// respawn, only when one is due: 32.03 B per particle plus ~19 % of groups' expiry lines at
+// C3.
 // ---------------------------------------------------------------------------------------
 // NTM: bit 0 = nontemporal loads, bit 1 = nontemporal stores.
 // Workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, "Workgroup
@@ -184,16 +185,31 @@ __device__ __forceinline__ void step_quad(const StreamArgs& a, att_ptr att0, siz
         asm volatile("" : "+v"(Eq));
         E = due ? Eq : h4{nx, nx, nx, nx};
       }
+      // The quad's particles that expire in this step, respawned one per pass of a mask loop:
+      // the wave runs one Philox pass whenever any of its 256 particles respawns (rarely two),
+      // not one per element slot (four inlined copies, each entered by ~19 % of waves at C3).
+      // Each particle's respawn is keyed by its own (gid, step), so the order is immaterial.
+      const uint16_t ck = (uint16_t)(clock0 + sub);
+      uint32_t m = 0;
 #pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        uint16_t e[2] = {E[2 * p], E[2 * p + 1]};
-        bool rr[2];
-        step_pair_life<LIFETIME>(a, step0 + sub, clock0 + sub, gid + 2 * p, x[p], y[p], vx[p], vy[p], e, rr);
-        E[2 * p] = e[0];
-        E[2 * p + 1] = e[1];
-        r[2 * p] |= rr[0];
-        r[2 * p + 1] |= rr[1];
-        any |= rr[0] | rr[1];
+      for (int c = 0; c < 4; ++c) m |= (E[c] == ck ? 1u : 0u) << c;
+      while (m) {
+        const uint32_t c = __builtin_ctz(m);
+        m &= m - 1u;
+        float px, py, qx, qy;
+        const uint32_t L = respawn(a, step0 + sub, gid + c, px, py, qx, qy);
+#pragma unroll
+        for (uint32_t cc = 0; cc < 4; ++cc) {
+          if (cc == c) {
+            x[cc >> 1][cc & 1] = px;
+            y[cc >> 1][cc & 1] = py;
+            vx[cc >> 1][cc & 1] = qx;
+            vy[cc >> 1][cc & 1] = qy;
+            E[cc] = (uint16_t)(ck + L);
+            r[cc] = true;
+          }
+        }
+        any = true;
       }
     }
   }
@@ -247,40 +263,60 @@ __device__ __forceinline__ void stream_body(const StreamArgs& a, att_ptr att0, s
   const uint64_t step0 = ((uint64_t)a.step_hi << 32) | a.step_lo;
   StatsAcc acc;
   if constexpr (STATS) acc.init();
-  for (uint64_t v = tid; v < nvec; v += stride) {
+  // Wave-uniform trip count (kBlock and the stride are multiples of 64): the lanes of a group
+  // fold their quads' next expiries across the 16-lane row after the body, so every lane of
+  // the wave takes part in the shuffles; lanes past the last quad skip the body.
+  for (uint64_t v = tid; (v & ~63ull) < nvec; v += stride) {
+    const bool valid = v < nvec;
     const uint64_t i = v << 2;
-    const uint64_t o = tidx(i);  // 4 consecutive particles never straddle a tile
-    // [next] is loaded first: the expiries of a due quad are then fetched while the state
-    // loads are still in flight (loads return in order).
     uint16_t nx = 0;
-    if constexpr (LIFETIME) nx = ldn<NTL>(a.next + nidx(i));
-    f4 X = ld4<NTL>(a.x + o);
-    f4 Y = ld4<NTL>(a.y + o);
-    f4 VX = ld4<NTL>(a.vx + o);
-    f4 VY = ld4<NTL>(a.vy + o);
-    h4 E = {0, 0, 0, 0}, Eq = {0, 0, 0, 0};
-    bool due = false;  // one of the quad's expiries falls in this launch's steps
-    if constexpr (LIFETIME) {
-      due = (uint16_t)(nx - (uint16_t)a.clock) < nsub;
-      // Every lane issues the expiry load; a lane with nothing due reads the first 8 B of the
-      // expiry segment instead (one cached line for the whole wave), so no bytes move for it.
-      Eq = *reinterpret_cast<const h4*>(a.exp + (due ? eidx(i) : 0));
-    }
-    bool re[4], any = false;
-    step_quad<VERLET, LIFETIME>(a, att0, att_stride, nsub, step0, a.clock, a.id_offset + i, X, Y, VX,
-                                VY, Eq, due, nx, E, re, any);
-    if constexpr (STATS) {
+    bool due = false;  // one of the group's expiries falls in this launch's steps (row-uniform)
+    uint32_t dn = 0x10000u;  // after the body: (u16)(quad's next expiry - end clock) if due
+    if (valid) {
+      const uint64_t o = tidx(i);  // 4 consecutive particles never straddle a tile
+      // [next] is loaded first: the expiries of a due group are then fetched while the state
+      // loads are still in flight (loads return in order).
+      if constexpr (LIFETIME) nx = ldn<NTL>(a.next + nidx(i));
+      f4 X = ld4<NTL>(a.x + o);
+      f4 Y = ld4<NTL>(a.y + o);
+      f4 VX = ld4<NTL>(a.vx + o);
+      f4 VY = ld4<NTL>(a.vy + o);
+      h4 E = {0, 0, 0, 0}, Eq = {0, 0, 0, 0};
+      if constexpr (LIFETIME) {
+        due = (uint16_t)(nx - (uint16_t)a.clock) < nsub;
+        // Every lane issues the expiry load; a lane with nothing due reads the first 8 B of
+        // the expiry segment instead (one cached line for the whole wave), so no bytes move
+        // for it.
+        Eq = *reinterpret_cast<const h4*>(a.exp + (due ? eidx(i) : 0));
+      }
+      bool re[4], any = false;
+      step_quad<VERLET, LIFETIME>(a, att0, att_stride, nsub, step0, a.clock, a.id_offset + i, X, Y,
+                                  VX, VY, Eq, due, nx, E, re, any);
+      if constexpr (STATS) {
 #pragma unroll
-      for (int c = 0; c < 4; ++c) acc.add(X[c], Y[c], VX[c], VY[c], re[c]);
+        for (int c = 0; c < 4; ++c) acc.add(X[c], Y[c], VX[c], VY[c], re[c]);
+      }
+      st4<NTS>(a.x + o, X);
+      st4<NTS>(a.y + o, Y);
+      st4<NTS>(a.vx + o, VX);
+      st4<NTS>(a.vy + o, VY);
+      if constexpr (LIFETIME) {
+        if (any) ste4<NTS>(a.exp + eidx(i), E);  // expiry written only on respawn
+        if (due) {
+          const uint16_t c1 = (uint16_t)(a.clock + nsub);
+          dn = (uint16_t)(quad_next(E[0], E[1], E[2], E[3], c1) - c1);
+        }
+      }
     }
-    st4<NTS>(a.x + o, X);
-    st4<NTS>(a.y + o, Y);
-    st4<NTS>(a.vx + o, VX);
-    st4<NTS>(a.vy + o, VY);
     if constexpr (LIFETIME) {
-      if (any) ste4<NTS>(a.exp + eidx(i), E);  // expiry written only on respawn
-      if (due) {
-        const uint16_t n2 = quad_next(E[0], E[1], E[2], E[3], (uint16_t)(a.clock + nsub));
+      // The group's next expiry: the nearest of its quads' (lanes past the last quad and
+      // groups not due hold 0x10000, which never wins in a due group).
+      dn = min(dn, (uint32_t)__shfl_xor((int)dn, 1, 16));
+      dn = min(dn, (uint32_t)__shfl_xor((int)dn, 2, 16));
+      dn = min(dn, (uint32_t)__shfl_xor((int)dn, 4, 16));
+      dn = min(dn, (uint32_t)__shfl_xor((int)dn, 8, 16));
+      if (due && (threadIdx.x & 15) == 0) {
+        const uint16_t n2 = (uint16_t)(a.clock + nsub + dn);
         if (n2 != nx) stn<NTS>(a.next + nidx(i), n2);
       }
     }
@@ -454,15 +490,24 @@ __global__ __launch_bounds__(kBlock) void life_scatter_kernel(uint16_t* exp, Lay
   exp[lidx(L, offset + j)] = (uint16_t)(clock + steps - 1u);
 }
 
-// [next] of quads [q0, q1) from their expiries at lifetime clock `clock` (after any write of
-// expiries outside the stream kernel: initial scatter, lifetime uploads).
+// [next] of groups [g0, g1) from the expiries of their full quads (quad index < nquads) at
+// lifetime clock `clock` (after any write of expiries outside the stream kernel: initial
+// scatter, lifetime uploads).
 __global__ __launch_bounds__(kBlock) void next_rebuild_kernel(const uint16_t* exp, uint16_t* next,
-                                                              uint64_t q0, uint64_t q1,
-                                                              uint32_t clock) {
-  const uint64_t q = q0 + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (q >= q1) return;
-  const h4 E = *reinterpret_cast<const h4*>(exp + eidx(q << 2));
-  next[nidx(q << 2)] = quad_next(E[0], E[1], E[2], E[3], (uint16_t)clock);
+                                                              uint64_t g0, uint64_t g1,
+                                                              uint64_t nquads, uint32_t clock) {
+  const uint64_t g = g0 + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (g >= g1) return;
+  const uint16_t c = (uint16_t)clock;
+  const uint64_t q0 = g << (kGroupLog - 2);
+  const uint64_t q1 = min(q0 + (kGroup >> 2), nquads);
+  uint16_t best = 0;
+  for (uint64_t q = q0; q < q1; ++q) {
+    const h4 E = *reinterpret_cast<const h4*>(exp + eidx(q << 2));
+    const uint16_t e = quad_next(E[0], E[1], E[2], E[3], c);
+    if (q == q0 || (uint16_t)(e - c) < (uint16_t)(best - c)) best = e;
+  }
+  next[nidx(g << kGroupLog)] = best;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1303,11 +1348,14 @@ hipError_t launch_field_scatter(float* field, Layout L, uint64_t offset, const f
 
 hipError_t launch_next_rebuild(const uint16_t* exp, uint16_t* next, uint64_t first, uint64_t n,
                                uint64_t total, uint32_t clock, hipStream_t s) {
-  // the full quads overlapping particles [first, first + n) of a shard of `total`
-  const uint64_t q0 = first >> 2, q1 = std::min((first + n + 3) >> 2, total >> 2);
-  if (n == 0 || q1 <= q0) return hipSuccess;
-  hipLaunchKernelGGL(next_rebuild_kernel, dim3(blocks_for(q1 - q0)), dim3(kBlock), 0, s, exp, next, q0,
-                     q1, clock);
+  // the groups overlapping particles [first, first + n) that hold a full quad of a shard of
+  // `total` particles
+  const uint64_t nquads = total >> 2;
+  const uint64_t g0 = first >> kGroupLog;
+  const uint64_t g1 = std::min((first + n + kGroup - 1) >> kGroupLog, (nquads * 4 + kGroup - 1) >> kGroupLog);
+  if (n == 0 || g1 <= g0) return hipSuccess;
+  hipLaunchKernelGGL(next_rebuild_kernel, dim3(blocks_for(g1 - g0)), dim3(kBlock), 0, s, exp, next, g0,
+                     g1, nquads, clock);
   return hipGetLastError();
 }
 

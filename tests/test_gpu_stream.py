@@ -234,7 +234,7 @@ def test_profiling_counts_dominant_kernel(gpu):
         ms, cnt = ctx.kernel_time()
         assert cnt == 7 and ms > 0
         amt, unit = ctx.step_cost()
-        assert unit == "bytes" and amt == 32.5 * n  # x, y, vx, vy r+w + the quads' [next] read
+        assert unit == "bytes" and amt == (32 + 2 / 64) * n  # x, y, vx, vy r+w + the groups' [next] read
         assert ctx.time_steps(3) > 0
 
 
