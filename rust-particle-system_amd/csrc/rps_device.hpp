@@ -293,21 +293,32 @@ __device__ __forceinline__ f2 inv_sqrt_nr(f2 r2) {
 
 // Sum of attractor accelerations at two particles (x, y), attractors in index order
 // (DESIGN.md §3.2).  att: this step's {x, y, strength, softening^2} (uniform, kernarg).
-__device__ __forceinline__ void attract2(att_ptr att, uint32_t na, f2 x, f2 y,
-                                         f2& ax, f2& ay) {
-  f2 sx = {0.0f, 0.0f}, sy = {0.0f, 0.0f};
+// NP pairs at once: their serial Newton chains interleave, so dependent v_pk_* ops of one
+// pair issue between those of the other instead of behind s_nop hazard padding.
+template <int NP>
+__device__ __forceinline__ void attract2(att_ptr att, uint32_t na, const f2 (&x)[NP],
+                                         const f2 (&y)[NP], f2 (&ax)[NP], f2 (&ay)[NP]) {
+  f2 sx[NP], sy[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) sx[p] = sy[p] = f2{0.0f, 0.0f};
   for (uint32_t k = 0; k < na; ++k) {
     const f4 A = att[k];
-    const f2 dx = A[0] - x;
-    const f2 dy = A[1] - y;
-    const f2 r2 = (dx * dx + dy * dy) + A[3];
-    const f2 inv = inv_sqrt_nr(r2);
-    const f2 s = A[2] * ((inv * inv) * inv);
-    sx = sx + dx * s;
-    sy = sy + dy * s;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const f2 dx = A[0] - x[p];
+      const f2 dy = A[1] - y[p];
+      const f2 r2 = (dx * dx + dy * dy) + A[3];
+      const f2 inv = inv_sqrt_nr(r2);
+      const f2 s = A[2] * ((inv * inv) * inv);
+      sx[p] = sx[p] + dx * s;
+      sy[p] = sy[p] + dy * s;
+    }
   }
-  ax = sx;
-  ay = sy;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    ax[p] = sx[p];
+    ay[p] = sy[p];
+  }
 }
 
 // Respawn at the emitter; returns the new lifetime in steps.
@@ -332,50 +343,68 @@ __device__ __forceinline__ uint32_t respawn(const StreamArgs& a, uint64_t step, 
 // step_pair_life (lifetime expiry and respawn, after the walls).  The kernels run the motion
 // of all their pairs before the lifetime part, so a quad's expiries -- loaded only when one
 // is due -- are needed last and their load overlaps the motion arithmetic.
-template <bool VERLET>
-__device__ __forceinline__ void step_pair_motion(const StreamArgs& a, att_ptr att, f2& x, f2& y,
-                                                 f2& vx, f2& vy) {
+template <bool VERLET, int NP>
+__device__ __forceinline__ void step_pair_motion(const StreamArgs& a, att_ptr att, f2 (&x)[NP],
+                                                 f2 (&y)[NP], f2 (&vx)[NP], f2 (&vy)[NP]) {
   const float dt = a.dt;
   if constexpr (!VERLET) {
-    vx = vx + a.gx_dt;  // apply_gravity, wgsl:397-400
-    vy = vy + a.gy_dt;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      vx[p] = vx[p] + a.gx_dt;  // apply_gravity, wgsl:397-400
+      vy[p] = vy[p] + a.gy_dt;
+    }
     if (a.na) {
-      f2 ax, ay;
-      attract2(att, a.na, x, y, ax, ay);
-      vx = vx + ax * dt;
-      vy = vy + ay * dt;
+      f2 ax[NP], ay[NP];
+      attract2<NP>(att, a.na, x, y, ax, ay);
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        vx[p] = vx[p] + ax[p] * dt;
+        vy[p] = vy[p] + ay[p] * dt;
+      }
     }
-    if (a.drag_on) {
-      vx = vx * a.drag_f;
-      vy = vy * a.drag_f;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      if (a.drag_on) {
+        vx[p] = vx[p] * a.drag_f;
+        vy[p] = vy[p] * a.drag_f;
+      }
+      x[p] = x[p] + vx[p] * dt;  // update_particle_positions, wgsl:392-395
+      y[p] = y[p] + vy[p] * dt;
     }
-    x = x + vx * dt;  // update_particle_positions, wgsl:392-395
-    y = y + vy * dt;
   } else {
-    f2 ax0, ay0, ax1, ay1;
-    attract2(att, a.na, x, y, ax0, ay0);
-    ay0 = ay0 + a.neg_g;
-    const f2 x1 = (x + vx * dt) + ax0 * a.half_dt2;
-    const f2 y1 = (y + vy * dt) + ay0 * a.half_dt2;
-    attract2(att, a.na, x1, y1, ax1, ay1);
-    ay1 = ay1 + a.neg_g;
-    vx = vx + (ax0 + ax1) * a.half_dt;
-    vy = vy + (ay0 + ay1) * a.half_dt;
-    if (a.drag_on) {
-      vx = vx * a.drag_f;
-      vy = vy * a.drag_f;
+    f2 ax0[NP], ay0[NP], ax1[NP], ay1[NP], x1[NP], y1[NP];
+    attract2<NP>(att, a.na, x, y, ax0, ay0);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      ay0[p] = ay0[p] + a.neg_g;
+      x1[p] = (x[p] + vx[p] * dt) + ax0[p] * a.half_dt2;
+      y1[p] = (y[p] + vy[p] * dt) + ay0[p] * a.half_dt2;
     }
-    x = x1;
-    y = y1;
+    attract2<NP>(att, a.na, x1, y1, ax1, ay1);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      ay1[p] = ay1[p] + a.neg_g;
+      vx[p] = vx[p] + (ax0[p] + ax1[p]) * a.half_dt;
+      vy[p] = vy[p] + (ay0[p] + ay1[p]) * a.half_dt;
+      if (a.drag_on) {
+        vx[p] = vx[p] * a.drag_f;
+        vy[p] = vy[p] * a.drag_f;
+      }
+      x[p] = x1[p];
+      y[p] = y1[p];
+    }
   }
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    float px = x[i], py = y[i], qx = vx[i], qy = vy[i];
-    wall(a.x_min, a.x_max, a.y_min, a.y_max, a.damping, px, py, qx, qy);
-    x[i] = px;
-    y[i] = py;
-    vx[i] = qx;
-    vy[i] = qy;
+  for (int p = 0; p < NP; ++p) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      float px = x[p][i], py = y[p][i], qx = vx[p][i], qy = vy[p][i];
+      wall(a.x_min, a.x_max, a.y_min, a.y_max, a.damping, px, py, qx, qy);
+      x[p][i] = px;
+      y[p][i] = py;
+      vx[p][i] = qx;
+      vy[p][i] = qy;
+    }
   }
 }
 
