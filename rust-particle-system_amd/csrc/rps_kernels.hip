@@ -1233,7 +1233,16 @@ uint32_t stream_blocks_for(uint64_t n) {
 
 template <bool V, bool L, bool S, int NTM>
 static hipError_t launch_stream_t(const StreamArgs& a, uint32_t grid, hipStream_t s) {
-  hipLaunchKernelGGL((stream_step_kernel<V, L, S, NTM>), dim3(grid), dim3(kBlock), 0, s, a);
+  // RPS_STREAM_LDS: LDS bytes reserved per workgroup and never used, an occupancy cap for
+  // experiments (default 0 = none).  28 000 B admits 5 workgroups per CU (5 waves/SIMD; 74
+  // VGPRs alone allow 6): 0.5084 -> 0.5059 ms per 1e8 step on one box, 0.5114 -> 0.5118 on
+  // another; 4 (32 KiB, 36 000 B) and 3 waves were 3 % and 11 % slower (tools/ab_stream.py).
+  static const uint32_t lds = [] {
+    const char* v = std::getenv("RPS_STREAM_LDS");
+    const long k = v && *v ? std::atol(v) : 0;
+    return (uint32_t)(k < 0 ? 0 : (k > 65536 ? 65536 : k));
+  }();
+  hipLaunchKernelGGL((stream_step_kernel<V, L, S, NTM>), dim3(grid), dim3(kBlock), lds, s, a);
   return hipGetLastError();
 }
 

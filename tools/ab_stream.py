@@ -1,6 +1,6 @@
 """Same-box A/B of librps builds on the C3 headline step (run on the GPU box).
 
-    python tools/ab_stream.py LIB_A LIB_B [...] [--rounds R] [--fuse K]
+    python tools/ab_stream.py LIB_A LIB_B[@ENV=VAL[@ENV2=VAL2]] [...] [--rounds R] [--fuse K]
 
 Each library runs in its own subprocess (one librps per process), in rounds A, B, A, B, ...
 so drift of the box (clocks, temperature) hits every variant alike.  One run: the bench's
@@ -53,14 +53,17 @@ def main():
     res = {l: [] for l in libs}
     for _ in range(rounds):
         for l in libs:
-            p = subprocess.run([sys.executable, __file__, "--one", l, str(fuse)], capture_output=True,
-                               text=True, timeout=300)
+            path, *envs = l.split("@")
+            env = dict(os.environ, **dict(e.split("=", 1) for e in envs))
+            p = subprocess.run([sys.executable, __file__, "--one", path, str(fuse)], capture_output=True,
+                               text=True, timeout=300, env=env)
             if p.returncode != 0:
                 print(p.stdout, p.stderr, flush=True)
                 sys.exit(p.returncode)
             line = p.stdout.strip().splitlines()[-1]
             print(line, flush=True)
             res[l].append(json.loads(line)["ms_per_step"])
+            print(json.dumps({"variant": l, "ms_per_step": res[l][-1]}), flush=True)
     print(json.dumps({"median_ms": {l: statistics.median(v) for l, v in res.items()}}), flush=True)
 
 

@@ -61,7 +61,7 @@ def main(tag):
                 traffic[WORKLOAD] = {"kernel": k, "FETCH_SIZE_KiB": d["FETCH_SIZE"], "WRITE_SIZE_KiB": d["WRITE_SIZE"],
                                      "hbm_bytes_per_launch": d["hbm_bytes_per_launch"],
                                      "algorithmic_bytes_per_launch": 40.0 * 1e8,
-                                     "moved_bytes_per_launch": 32.5 * 1e8,
+                                     "moved_bytes_per_launch": (32.0 + 2.0 / 64) * 1e8,
                                      "correction": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE = 1/2 of wide-stream bytes)",
                                      "round": tag}
     with open(os.path.join(PROF, f"{tag}_kernel_summary.json"), "w") as f:
