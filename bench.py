@@ -4,8 +4,8 @@
 Workload (BASELINE.json configs[2]): 1e8 particles per GPU, 4 attractors
 moving on circles, drag, lifetime decay + Philox respawn, semi-implicit Euler, walls.  One
 "step" = one fused stream-kernel launch over every particle (in place, tiled SoA; 40 B per
-particle of algorithmic traffic per SURVEY §8(d), of which the kernel moves 32.5: x, y, vx, vy
-read+written and a u16 per quad of particles naming its earliest lifetime expiry).  Multi-GPU: one process per GPU, contiguous index shards with global particle ids, no
+particle of algorithmic traffic per SURVEY §8(d), of which the kernel moves 32.03: x, y, vx, vy
+read+written and a u16 per group of 64 particles naming its earliest lifetime expiry).  Multi-GPU: one process per GPU, contiguous index shards with global particle ids, no
 data-path collective (weak scaling: 1e8 particles per rank).  Side lines: "sph", the
 reference's five-pass SPH frame at 2^22 particles (replicas); "allpairs", the all-pairs
 N-body step with its RCCL all-gather, strong-scaled over the ranks.
@@ -28,8 +28,9 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 METRIC = "particle-updates/sec + achieved HBM GB/s, 10^8 particles, 1/2/4/8 MI355X"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # SURVEY.md §8(d) / BASELINE.md, C3: the algorithmic cost of a particle-step is 40 B (read and
-# write x, y, vx, vy and an f32 lifetime).  The kernel moves 32.5 of them (the lifetime is a u16
-# expiry read and written only in the quad-steps where one is due, found from a u16 per quad:
+# write x, y, vx, vy and an f32 lifetime).  The kernel moves 32.03 of them (the lifetime is a u16
+# expiry read and written only in the group-steps where one is due, found from a u16 per group
+# of 64 particles:
 # DESIGN.md §3.2, §4): that figure is reported beside it as `moved_*`, and `traffic` is what
 # the PMC counters measured.
 ALGO_BYTES_PER_PARTICLE = 40.0
@@ -301,7 +302,7 @@ def main():
     elapsed = d.max(t1 - t0)
     kern_ms, launches = ctx.kernel_time()
     kern_ms = d.max(kern_ms)
-    moved_per_launch, _ = ctx.step_cost()  # bytes the kernel moves: 32.5 B per particle
+    moved_per_launch, _ = ctx.step_cost()  # bytes the kernel moves: 32.03 B per particle
     algo_per_launch = ALGO_BYTES_PER_PARTICLE * n
     st = ctx.stats()
     ctx.close()
