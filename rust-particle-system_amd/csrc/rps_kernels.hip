@@ -803,10 +803,12 @@ __device__ __forceinline__ uint32_t sort_chunk(const PaddedTile& s, uint32_t off
     uint32_t b, r;
     sort_group_at(q, G, g, flip, b, r);
     if (flip) {
-      if (KMAX >= 3 && K == 2u) sort_group<2, true>(s, off + b, r, g);
+      if (KMAX >= 4 && K == 3u) sort_group<3, true>(s, off + b, r, g);
+      else if (KMAX >= 3 && K == 2u) sort_group<2, true>(s, off + b, r, g);
       else sort_group<1, true>(s, off + b, r, g);
     } else {
-      if (KMAX >= 3 && K == 3u) sort_group<3, false>(s, off + b, r, g);
+      if (KMAX >= 4 && K == 4u) sort_group<4, false>(s, off + b, r, g);
+      else if (KMAX >= 3 && K == 3u) sort_group<3, false>(s, off + b, r, g);
       else if (KMAX >= 2 && K == 2u) sort_group<2, false>(s, off + b, r, g);
       else sort_group<1, false>(s, off + b, r, g);
     }
@@ -1451,11 +1453,13 @@ static hipError_t launch_sort_local(int kmax, bool bin, uint32_t tiles, uint32_t
     hipLaunchKernelGGL((sph_sort_local_kernel<B, K>), dim3(tiles), dim3(threads), 0, s, lookup,  \
                        tile, lo, hi, first, sb)
   if (bin) {
-    if (kmax == 3) RPS_LOCAL(true, 3);
+    if (kmax == 4) RPS_LOCAL(true, 4);
+    else if (kmax == 3) RPS_LOCAL(true, 3);
     else if (kmax == 2) RPS_LOCAL(true, 2);
     else RPS_LOCAL(true, 1);
   } else {
-    if (kmax == 3) RPS_LOCAL(false, 3);
+    if (kmax == 4) RPS_LOCAL(false, 4);
+    else if (kmax == 3) RPS_LOCAL(false, 3);
     else if (kmax == 2) RPS_LOCAL(false, 2);
     else RPS_LOCAL(false, 1);
   }
@@ -1474,7 +1478,7 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
   static const int kmax_env = [] {
     const char* v = std::getenv("RPS_SORT_KMAX");
     const int k = v && *v ? std::atoi(v) : 0;  // 0: by tile size (below)
-    return k < 0 ? 0 : (k > 3 ? 3 : k);
+    return k < 0 ? 0 : (k > 4 ? 4 : k);
   }();
   const SortBin bin{b.cfg, b.st, b.offsets, b.n};
   const SortBin nobin{nullptr, nullptr, nullptr, 0u};
@@ -1484,8 +1488,11 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
     ++*launches;
     return hipGetLastError();
   }
-  // Tile: 2048 entries up to P = 2^18 (enough workgroups to fill the chip in the LDS
-  // passes), 8192 above (fewer global passes; measured at 50 k / 1 M / 4 M particles).
+  // Tile: P / 256 entries clamped to [2048, 8192] -- one workgroup per CU in the LDS passes
+  // once P allows it, and the largest such tile (fewest global passes).  Measured per size
+  // (tools/kmax_sweep.sh): 2048 up to P = 2^19, 4096 at 2^20, 8192 from 2^21.
+  // A fixed 8192 above 2^18 left half the CUs idle at 2^20 (0.429 -> 0.404 ms/frame) and
+  // 2^19 (0.294 -> 0.265).
   static const uint32_t tile_env = [] {
     const char* v = std::getenv("RPS_SORT_TILE");
     const uint32_t t = v && *v ? (uint32_t)std::atoi(v) : 0u;
@@ -1496,10 +1503,10 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
     const int k = v && *v ? std::atoi(v) : 4;
     return (uint32_t)(k < 1 ? 1 : (k > 5 ? 5 : k));
   }();
-  const uint32_t want = tile_env ? tile_env : (P <= (1u << 18) ? 2048u : kSortTile);
+  const uint32_t want = tile_env ? tile_env : std::min(kSortTile, std::max(2048u, P / 256u));
   const uint32_t tile = P < want ? P : want;
-  // Passes per register chunk: 3 on 8192-entry tiles, 2 on smaller ones (measured at 65 536,
-  // 2^20 and 2^22 particles).
+  // Passes per register chunk: 3 on 8192-entry tiles, 2 on smaller ones (measured at 65 536
+  // to 2^22 particles; 4 is slower everywhere: fewer waves per CU).
   const int kmax = kmax_env ? kmax_env : (tile >= kSortTile ? 3 : 2);
   uint32_t tile_log = 0;
   while ((1u << tile_log) < tile) ++tile_log;
