@@ -1554,13 +1554,24 @@ hipError_t launch_sph_offsets(const SphBuffers& b, hipStream_t s) {
   return hipGetLastError();
 }
 
-static int sph_batch() {
-  static const int b = [] {
-    const char* v = std::getenv("RPS_SPH_BATCH");
-    const int k = v && *v ? std::atoi(v) : 8;
-    return k == 4 || k == 16 ? k : 8;
-  }();
-  return b;
+// Entries in flight per lane in the density (`d`) and sim scans: RPS_SPH_BATCH_D /
+// RPS_SPH_BATCH_S, else RPS_SPH_BATCH, else by size (measured).
+static int sph_env_batch(const char* name) {
+  const char* v = std::getenv(name);
+  const int k = v && *v ? std::atoi(v) : 0;
+  return k == 4 || k == 8 || k == 16 ? k : 0;
+}
+static int sph_batch(bool density, uint32_t p) {
+  static const int both = sph_env_batch("RPS_SPH_BATCH");
+  static const int d = sph_env_batch("RPS_SPH_BATCH_D");
+  static const int sim = sph_env_batch("RPS_SPH_BATCH_S");
+  const int k = density ? d : sim;
+  if (k) return k;
+  if (both) return both;
+  // The sim scan keeps 4 entries in flight up to P = 2^21, where its slot records stay in
+  // the caches (2^20 frame 0.404 -> 0.392 ms, 2^21 0.670 -> 0.651), and 8 beyond (2^22: 1.25
+  // vs 1.28 ms with 4).  The density scan is indifferent (4 or 8 within 0.3 %).
+  return density || p > (1u << 21) ? 8 : 4;
 }
 
 hipError_t launch_sph_pre(const SphBuffers& b, hipStream_t s) {
@@ -1571,7 +1582,7 @@ hipError_t launch_sph_pre(const SphBuffers& b, hipStream_t s) {
 #define RPS_DENSITY(B)                                                                           \
   hipLaunchKernelGGL(sph_density_kernel<B>, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg, \
                      b.offsets, b.ends, b.sl, b.p)
-  switch (sph_batch()) {
+  switch (sph_batch(true, b.p)) {
     case 4: RPS_DENSITY(4); break;
     case 16: RPS_DENSITY(16); break;
     default: RPS_DENSITY(8); break;
@@ -1588,7 +1599,7 @@ hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s) {
   else                                                                                         \
     hipLaunchKernelGGL((sph_sim_kernel<B, true>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s,   \
                        b.cfg, b.offsets, b.ends, b.sl, b.st2, b.p)
-  switch (sph_batch()) {
+  switch (sph_batch(false, b.p)) {
     case 4: RPS_SIM(4); break;
     case 16: RPS_SIM(16); break;
     default: RPS_SIM(8); break;
