@@ -837,13 +837,30 @@ __device__ __forceinline__ void wave_lds_sync() {
 template <bool BIN, int KMAX, uint32_t CAP = kSortTile>
 __global__ __launch_bounds__(1024) void sph_sort_local_kernel(
     uint2* __restrict__ lookup, uint32_t tile, uint32_t stage_lo, uint32_t stage_hi,
-    uint32_t first_step, SortBin bin) {
+    uint32_t first_step, SortBin bin, uint32_t vec) {
   __shared__ uint2 lds[CAP + CAP / 32];
   const PaddedTile s{lds};
   const uint32_t base0 = blockIdx.x * tile;
-  for (uint32_t q = threadIdx.x; q < tile; q += blockDim.x) {
-    const uint32_t gq = base0 + q;
-    s[q] = (BIN && gq < bin.n) ? bin_entry(bin, gq) : lookup[gq];
+  if (vec) {  // two entries per lane: 16-B global loads (tile is even, base0 16-B aligned)
+    for (uint32_t q = 2u * threadIdx.x; q < tile; q += 2u * blockDim.x) {
+      const uint32_t gq = base0 + q;
+      uint2 a, c;
+      if (BIN && gq < bin.n) {
+        a = bin_entry(bin, gq);
+        c = gq + 1u < bin.n ? bin_entry(bin, gq + 1u) : lookup[gq + 1u];
+      } else {
+        const uint4 v = *reinterpret_cast<const uint4*>(lookup + gq);
+        a = make_uint2(v.x, v.y);
+        c = make_uint2(v.z, v.w);
+      }
+      s[q] = a;
+      s[q + 1u] = c;
+    }
+  } else {
+    for (uint32_t q = threadIdx.x; q < tile; q += blockDim.x) {
+      const uint32_t gq = base0 + q;
+      s[q] = (BIN && gq < bin.n) ? bin_entry(bin, gq) : lookup[gq];
+    }
   }
   __syncthreads();
   const uint32_t ws = min(tile, 64u << KMAX);  // one wave's span (blockDim is a multiple of 64)
@@ -868,7 +885,14 @@ __global__ __launch_bounds__(1024) void sph_sort_local_kernel(
     stage = last + 1u;
     step = 0u;
   }
-  for (uint32_t q = threadIdx.x; q < tile; q += blockDim.x) lookup[base0 + q] = s[q];
+  if (vec) {
+    for (uint32_t q = 2u * threadIdx.x; q < tile; q += 2u * blockDim.x) {
+      const uint2 a = s[q], c = s[q + 1u];
+      *reinterpret_cast<uint4*>(lookup + base0 + q) = make_uint4(a.x, a.y, c.x, c.y);
+    }
+  } else {
+    for (uint32_t q = threadIdx.x; q < tile; q += blockDim.x) lookup[base0 + q] = s[q];
+  }
 }
 
 // calculate_spatial_lookup_offsets, compute_shader.wgsl:507-525: offsets[key] = the first
@@ -1448,10 +1472,16 @@ static hipError_t launch_sort_local(int kmax, bool bin, uint32_t tiles, uint32_t
 #define RPS_LOCAL(B, K)                                                                          \
   if (tile > kSortTile)                                                                          \
     hipLaunchKernelGGL((sph_sort_local_kernel<B, K, kSortTileMax>), dim3(tiles), dim3(threads), 0, \
-                       s, lookup, tile, lo, hi, first, sb);                                      \
+                       s, lookup, tile, lo, hi, first, sb, vec);                                 \
   else                                                                                           \
     hipLaunchKernelGGL((sph_sort_local_kernel<B, K>), dim3(tiles), dim3(threads), 0, s, lookup,  \
-                       tile, lo, hi, first, sb)
+                       tile, lo, hi, first, sb, vec)
+  // 16-B tile loads/stores (RPS_SORT_VEC=0: 8-B, one entry per lane).
+  static const uint32_t vec_env = [] {
+    const char* v = std::getenv("RPS_SORT_VEC");
+    return (v && *v) ? (uint32_t)(std::atoi(v) != 0) : 1u;
+  }();
+  const uint32_t vec = (tile >= 2u) ? vec_env : 0u;
   if (bin) {
     if (kmax == 4) RPS_LOCAL(true, 4);
     else if (kmax == 3) RPS_LOCAL(true, 3);
@@ -1484,7 +1514,7 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
   const SortBin nobin{nullptr, nullptr, nullptr, 0u};
   if (stages == 0) {  // P == 1: nothing to sort, only bin
     hipLaunchKernelGGL((sph_sort_local_kernel<true, 1>), dim3(1), dim3(64), 0, s, b.lookup, 1u, 1u, 0u,
-                       0u, bin);
+                       0u, bin, 0u);
     ++*launches;
     return hipGetLastError();
   }
