@@ -416,16 +416,18 @@ int step_nbody(rps_ctx* ctx) {
   return RPS_OK;
 }
 
-int step_sph_grid(rps_ctx* ctx) {
+// Passes 1-3.  On an active frame the offsets pass (3) rides in pass 4's first kernel
+// instead (fold_offsets): nothing between them reads offsets/ends.
+int step_sph_grid(rps_ctx* ctx, bool fold_offsets) {
   SphBuffers b = sph_buffers(ctx);
   RPS_HIP(ctx, launch_sph_sort(b, ctx->stream, &ctx->sort_passes, &ctx->sort_launches));
-  RPS_HIP(ctx, launch_sph_offsets(b, ctx->stream));
+  if (!fold_offsets) RPS_HIP(ctx, launch_sph_offsets(b, ctx->stream));
   return RPS_OK;
 }
 
-int step_sph_sim(rps_ctx* ctx) {
+int step_sph_sim(rps_ctx* ctx, bool with_offsets) {
   SphBuffers b = sph_buffers(ctx);
-  RPS_HIP(ctx, launch_sph_pre(b, ctx->stream));
+  RPS_HIP(ctx, launch_sph_pre(b, ctx->stream, with_offsets));
   int rc = prof_begin(ctx);
   if (rc) return rc;
   RPS_HIP(ctx, launch_sph_sim(b, ctx->stream));
@@ -889,7 +891,8 @@ int rps_step(rps_ctx* ctx, uint32_t nsteps) {
     ctx->cfg.frame_count += 1;  // src/particle_buffers.rs:227
     const bool active = ctx->cfg.frame_count >= ctx->ext.shader_delay;  // wgsl:426, :442
     if (ctx->mode == RPS_MODE_SPH) {
-      rc = step_sph_grid(ctx);  // passes 1-3 run every frame (particle_compute.rs:105-163)
+      // passes 1-3 run every frame (particle_compute.rs:105-163)
+      rc = step_sph_grid(ctx, active && sph_fold_offsets());
       if (rc) return rc;
     }
     if (!active) continue;
@@ -914,7 +917,7 @@ int rps_step(rps_ctx* ctx, uint32_t nsteps) {
     switch (ctx->mode) {
       case RPS_MODE_STREAM: rc = step_stream(ctx); break;
       case RPS_MODE_NBODY: rc = step_nbody(ctx); break;
-      default: rc = step_sph_sim(ctx); break;
+      default: rc = step_sph_sim(ctx, sph_fold_offsets()); break;
     }
     if (rc) return rc;
     ++ctx->active_steps;

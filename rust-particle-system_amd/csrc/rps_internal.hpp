@@ -117,7 +117,10 @@ struct SphBuffers {
 hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
                            uint32_t* launches);
 hipError_t launch_sph_offsets(const SphBuffers& b, hipStream_t s);
-hipError_t launch_sph_pre(const SphBuffers& b, hipStream_t s);
+// with_offsets: the predict kernel also runs the offsets pass (it needs only the sorted
+// lookup), saving a launch on active frames; see sph_fold_offsets (RPS_SPH_FOLD_OFFSETS=0: off).
+hipError_t launch_sph_pre(const SphBuffers& b, hipStream_t s, bool with_offsets);
+bool sph_fold_offsets();
 hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s);
 // Rebuild the per-particle predicted-position and density buffers from the slot records.
 hipError_t launch_sph_debug_views(const SphBuffers& b, hipStream_t s);

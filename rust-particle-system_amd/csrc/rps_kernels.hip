@@ -928,10 +928,20 @@ __constant__ int32_t kGridOff[9][2] = {{-1, -1}, {-1, 0}, {-1, 1}, {0, -1}, {0, 
 __global__ __launch_bounds__(kBlock) void sph_predict_kernel(const rps_config* __restrict__ cfg,
                                                              const uint2* __restrict__ lookup,
                                                              const f4* __restrict__ st,
-                                                             SphSlots sl, uint32_t p_slots) {
+                                                             SphSlots sl, uint32_t p_slots,
+                                                             uint32_t* __restrict__ offsets,
+                                                             uint32_t* __restrict__ ends,
+                                                             uint32_t n_offsets) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= p_slots) return;
-  const uint32_t i = lookup[t].y;
+  const uint2 e = lookup[t];
+  if (t < n_offsets) {  // the offsets pass folded in (active frames): sph_offsets_kernel's body
+    const uint32_t prev = t > 0u ? lookup[t - 1u].x : 0xFFFFFFFFu;
+    const uint32_t next = t + 1u < n_offsets ? lookup[t + 1u].x : 0xFFFFFFFFu;
+    if (e.x != prev) offsets[e.x] = t;
+    if (e.x != next || t + 1u == n_offsets) ends[e.x] = t + 1u;
+  }
+  const uint32_t i = e.y;
   const f4 s = st[i];
   const float dt = cfg->fixed_delta_time;
   const float qx = s[2] + 0.0f * dt;  // apply_gravity, wgsl:397-400
@@ -1604,9 +1614,17 @@ static int sph_batch(bool density, uint32_t p) {
   return density || p > (1u << 21) ? 8 : 4;
 }
 
-hipError_t launch_sph_pre(const SphBuffers& b, hipStream_t s) {
+bool sph_fold_offsets() {
+  static const bool f = [] {
+    const char* v = std::getenv("RPS_SPH_FOLD_OFFSETS");
+    return !(v && *v && std::atoi(v) == 0);
+  }();
+  return f;
+}
+
+hipError_t launch_sph_pre(const SphBuffers& b, hipStream_t s, bool with_offsets) {
   hipLaunchKernelGGL(sph_predict_kernel, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg, b.lookup,
-                     b.st, b.sl, b.p);
+                     b.st, b.sl, b.p, b.offsets, b.ends, with_offsets ? b.n : 0u);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
 #define RPS_DENSITY(B)                                                                           \
