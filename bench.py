@@ -13,6 +13,10 @@ N-body step with its RCCL all-gather, strong-scaled over the ranks.
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
+A plain `python bench.py --gpus N` (N > 1, no WORLD_SIZE in the environment) starts the N ranks
+itself through torch.distributed.run as a child process, before any GPU call, and exits with
+its status.  Under a launcher, `--gpus` must equal WORLD_SIZE (exit 2 otherwise).
+
 Prints ONE JSON line on rank 0 (fields: see the contract in DESIGN.md §6).
 """
 import argparse
@@ -59,8 +63,31 @@ def parse():
                     help="particles of the SPH CPU-baseline sample (oracle, one thread)")
     ap.add_argument("--sph-cpu-frames", type=int, default=3)
     ap.add_argument("--allpairs-timeout", type=float, default=240.0,
-                    help="watchdog: print the headline line and exit if the side run hangs")
+                    help="watchdog: print the headline line and exit non-zero if a side run hangs")
+    ap.add_argument("--master-port", type=int, default=0,
+                    help="rendezvous port when bench.py starts its own ranks (0: a free port)")
     return ap.parse_args()
+
+
+WATCHDOG_RC = 3  # a side run hung: the headline line is printed, the process still fails
+STATS_MISMATCH_RC = 4  # librps's RCCL stats all-reduce disagrees with torch.distributed's
+
+
+def launch_ranks(args) -> int:
+    """`--gpus N` without a launcher: run N ranks of this script under torch.distributed.run
+    (one process per GPU, rendezvous on 127.0.0.1) as a child process.  Nothing here touches
+    the GPU, so the ranks own their devices."""
+    import socket
+    import subprocess
+
+    port = args.master_port
+    if not port:
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
 
 
 class Dist:
@@ -119,6 +146,16 @@ class Dist:
     def close(self):
         if self.dist:
             self.dist.destroy_process_group()
+
+
+def load_impl():
+    """The library binding.  RPS_BENCH_TEST_STUB names a CPU test double of rps_amd, and only
+    tests/test_bench_launcher.py sets it (launcher, aggregation and watchdog checks without a
+    GPU); every real run loads the HIP library, which fails loudly when it is missing."""
+    import importlib
+
+    stub = os.environ.get("RPS_BENCH_TEST_STUB")
+    return importlib.import_module(stub) if stub else importlib.import_module("rps_amd")
 
 
 def workload(rps, n_rank, world):
@@ -275,10 +312,30 @@ def sph_cpu_baseline(rps, args):
                       f"one thread), {el:.1f} s; {el * 1e3 / args.sph_cpu_frames:.0f} ms/frame"}
 
 
+def stats_check(d, st_all, st_shard):
+    """With more than one rank the stream context holds an RCCL communicator, and librps
+    all-reduces every stats step itself (rps_get_stats).  Its result must equal the same
+    combination of the shard stats (rps_get_shard_stats) done by torch.distributed."""
+    ref = global_stats(d, st_shard)
+    lib = {"bbox": list(st_all.bbox), "kinetic_energy": st_all.kinetic_energy,
+           "respawned_last": int(st_all.respawned), "particles": int(st_all.particles)}
+    ok = (lib["bbox"] == ref["bbox"] and lib["particles"] == ref["particles"]
+          and lib["respawned_last"] == ref["respawned_last"]
+          and abs(lib["kinetic_energy"] - ref["kinetic_energy"]) <= 1e-12 * abs(ref["kinetic_energy"]))
+    ref["librps_rccl_allreduce"] = "matches torch.distributed" if ok else {"mismatch": lib}
+    return ref, ok
+
+
 def main():
     args = parse()
+    launched = "WORLD_SIZE" in os.environ
+    if args.gpus > 1 and not launched:
+        sys.exit(launch_ranks(args))
     d = Dist()
-    import rps_amd as rps
+    if d.world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started {d.world} rank(s)", file=sys.stderr)
+        sys.exit(2)
+    rps = load_impl()
 
     n = args.particles
     cfg, ext = workload(rps, n, d.world)
@@ -286,6 +343,8 @@ def main():
     ctx = rps.Context(n, rps.MODE_STREAM, device=d.local if d.dist else 0,
                       id_offset=d.rank * n, global_count=d.world * n)
     ctx.set_config(cfg, ext)
+    if d.world > 1:  # the stats steps all-reduce over the ranks inside librps (RCCL)
+        ctx.comm_init(d.rank, d.world, d.broadcast_bytes(rps.comm_unique_id() if d.rank == 0 else b""))
     ctx.init_scatter(args.seed)
     ctx.step(args.warmup)
     ctx.sync()
@@ -304,7 +363,10 @@ def main():
     kern_ms = d.max(kern_ms)
     moved_per_launch, _ = ctx.step_cost()  # bytes the kernel moves: 32.03 B per particle
     algo_per_launch = ALGO_BYTES_PER_PARTICLE * n
-    st = ctx.stats()
+    if d.world > 1:
+        stats, stats_ok = stats_check(d, ctx.stats(), ctx.shard_stats())
+    else:
+        stats, stats_ok = global_stats(d, ctx.stats()), True
     ctx.close()
 
     updates = float(n) * d.world * args.steps
@@ -337,7 +399,7 @@ def main():
                      "algorithmic_bytes_per_launch": algo_per_launch,
                      "moved_bytes_per_launch": moved_per_launch, "moved_gbps": moved_gbps,
                      "moved_frac": moved_gbps / HBM_PEAK_GBPS},
-        "stats": global_stats(d, st),
+        "stats": stats,
     }
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(rps, args, cfg, ext)
@@ -347,11 +409,12 @@ def main():
             continue
         import threading
 
-        def _watchdog(key=key):  # a hung side run must not cost the headline line
+        def _watchdog(key=key):  # a hung side run must not cost the headline line, but fails the run
             if d.rank == 0:
                 line[key] = {"error": f"watchdog: no result within {args.allpairs_timeout} s"}
                 print(json.dumps(line), flush=True)
-            os._exit(0)
+            print(f"bench.py: side run '{key}' hung; exiting {WATCHDOG_RC}", file=sys.stderr, flush=True)
+            os._exit(WATCHDOG_RC)
 
         timer = threading.Timer(args.allpairs_timeout, _watchdog)
         timer.daemon = True
@@ -364,6 +427,9 @@ def main():
     if d.rank == 0:
         print(json.dumps(line), flush=True)
     d.close()
+    if not stats_ok:
+        print("bench.py: librps stats all-reduce != torch.distributed", file=sys.stderr)
+        sys.exit(STATS_MISMATCH_RC)
 
 
 if __name__ == "__main__":

@@ -243,6 +243,9 @@ int rps_sync(rps_ctx* ctx);
  * communicator (rps_comm_init, STREAM mode) they cover every rank's shard: each stats step
  * all-reduces bbox min/max and the KE / particle / respawn sums over the ranks (RCCL). */
 int rps_get_stats(rps_ctx* ctx, rps_stats* out);
+/* The same stats step over this rank's shard only (no reduction over the ranks), so a host
+ * can check the library's RCCL all-reduce against its own transport (bench.py). */
+int rps_get_shard_stats(rps_ctx* ctx, rps_stats* out);
 
 /* Host-visible counters: frame_count of the device config and active steps executed. */
 int rps_get_counters(const rps_ctx* ctx, uint32_t* frame_count, uint64_t* active_steps);

@@ -937,22 +937,23 @@ int rps_sync(rps_ctx* ctx) {
   return RPS_OK;
 }
 
-int rps_get_stats(rps_ctx* ctx, rps_stats* out) {
+static int get_stats(rps_ctx* ctx, rps_stats* out, bool all_ranks) {
   int rc = check_ctx(ctx);
   if (rc) return rc;
   if (!out) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "null output");
   if (!ctx->have_stats) return fail(ctx, RPS_ERR_UNSUPPORTED, "no stats reduced yet (RPS_EXT_STATS)");
   StatsResult r;
   StatsGlobal g;
+  const bool global = all_ranks && ctx->comm;
   RPS_HIP(ctx, hipMemcpyAsync(&r, ctx->d_stats, sizeof(r), hipMemcpyDeviceToHost, ctx->stream));
-  if (ctx->comm) RPS_HIP(ctx, hipMemcpyAsync(&g, ctx->d_gstats, sizeof(g), hipMemcpyDeviceToHost, ctx->stream));
+  if (global) RPS_HIP(ctx, hipMemcpyAsync(&g, ctx->d_gstats, sizeof(g), hipMemcpyDeviceToHost, ctx->stream));
   RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
   for (int k = 0; k < 4; ++k) out->bbox[k] = r.bbox[k];
   out->kinetic_energy = r.ke;
   out->particles = r.count;
   out->respawned = r.respawned;
   out->step = r.step;
-  if (ctx->comm) {  // every rank's shard (allreduce_stats)
+  if (global) {  // every rank's shard (allreduce_stats)
     out->bbox[0] = -g.neg_min_max[0];
     out->bbox[1] = g.neg_min_max[1];
     out->bbox[2] = -g.neg_min_max[2];
@@ -963,6 +964,9 @@ int rps_get_stats(rps_ctx* ctx, rps_stats* out) {
   }
   return RPS_OK;
 }
+
+int rps_get_stats(rps_ctx* ctx, rps_stats* out) { return get_stats(ctx, out, true); }
+int rps_get_shard_stats(rps_ctx* ctx, rps_stats* out) { return get_stats(ctx, out, false); }
 
 int rps_get_counters(const rps_ctx* ctx, uint32_t* frame_count, uint64_t* active_steps) {
   if (!ctx) return fail(nullptr, RPS_ERR_INVALID_ARGUMENT, "null context");

@@ -173,6 +173,7 @@ ABI_SYMBOLS = [
     ("rps_update", _I, [_P]),
     ("rps_sync", _I, [_P]),
     ("rps_get_stats", _I, [_P, ctypes.POINTER(Stats)]),
+    ("rps_get_shard_stats", _I, [_P, ctypes.POINTER(Stats)]),
     ("rps_get_counters", _I, [_P, ctypes.POINTER(_U32), ctypes.POINTER(_U64)]),
     ("rps_set_profiling", _I, [_P, _I]),
     ("rps_get_kernel_time", _I, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64)]),
@@ -485,6 +486,12 @@ class Context:
     def stats(self) -> Stats:
         s = Stats()
         self._call("rps_get_stats", ctypes.byref(s))
+        return s
+
+    def shard_stats(self) -> Stats:
+        """This rank's shard only, even with a communicator (rps_get_shard_stats)."""
+        s = Stats()
+        self._call("rps_get_shard_stats", ctypes.byref(s))
         return s
 
     def counters(self):
