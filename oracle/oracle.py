@@ -39,6 +39,7 @@ def lib(omp: bool = False) -> ctypes.CDLL:
     sig = {
         "orc_philox4x32_10": (None, [_P, _P, _P]),
         "orc_sincos_turns": (None, [_F, ctypes.POINTER(_F), ctypes.POINTER(_F)]),
+        "orc_log_unit": (_F, [_F]),
         "orc_attractor_pos": (None, [_P, ctypes.c_double, ctypes.POINTER(_F), ctypes.POINTER(_F)]),
         "orc_set_color": (None, [_F, _F, _F, _P]),
         "orc_hash_cell": (_U32, [ctypes.c_int32, ctypes.c_int32]),
@@ -87,6 +88,10 @@ def sincos_turns(u):
     c, s = ctypes.c_float(), ctypes.c_float()
     lib().orc_sincos_turns(u, ctypes.byref(c), ctypes.byref(s))
     return c.value, s.value
+
+
+def log_unit(u):
+    return lib().orc_log_unit(u)
 
 
 def set_color(vx, vy, max_energy):

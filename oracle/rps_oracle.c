@@ -77,6 +77,36 @@ void orc_sincos_turns(float u, float* c_out, float* s_out) {
   }
 }
 
+/* ln(u) for normal u in (0, 1]: exponent split by bit operations, then the atanh series
+ * ln m = 2s(1 + s^2/3 + ... + s^14/15), s = (m-1)/(m+1), m in [sqrt(1/2), sqrt(2)).  Exact
+ * bit operations and fixed-order +, *, / only, so the HIP kernel (log_unit) reproduces it bit
+ * for bit where glibc logf and the device logf differ in the last bit. */
+float orc_log_unit(float u) {
+  uint32_t b;
+  memcpy(&b, &u, 4);
+  int e = (int)((b >> 23) & 255u) - 127;
+  uint32_t mb = (b & 0x007fffffu) | 0x3f800000u;
+  float m;
+  memcpy(&m, &mb, 4);
+  if (m > 1.41421356f) {
+    m = m * 0.5f;
+    e = e + 1;
+  }
+  float s = (m - 1.0f) / (m + 1.0f);
+  float s2 = s * s;
+  float p = 6.66666666666666667e-02f;     /* 1/15 */
+  p = p * s2 + 7.69230769230769231e-02f;  /* 1/13 */
+  p = p * s2 + 9.09090909090909091e-02f;  /* 1/11 */
+  p = p * s2 + 1.11111111111111111e-01f;  /* 1/9  */
+  p = p * s2 + 1.42857142857142857e-01f;  /* 1/7  */
+  p = p * s2 + 2.00000000000000000e-01f;  /* 1/5  */
+  p = p * s2 + 3.33333333333333333e-01f;  /* 1/3  */
+  float t = s + s;
+  float lnm = t + t * (s2 * p);
+  float ef = (float)e;
+  return ef * 6.93145751953125e-01f + (ef * 1.42860682030941723e-06f + lnm);
+}
+
 void orc_attractor_pos(const rps_attractor* a, double t, float* px, float* py) {
   double ang = (double)a->angular_velocity * t + (double)a->phase;
   *px = (float)((double)a->center[0] + (double)a->orbit_radius * cos(ang));
@@ -420,7 +450,7 @@ void orc_init_scatter(const rps_config* cfg, const rps_ext_config* ext, uint64_t
     float u1 = (float)((w[0] >> 8) + 1u) * (1.0f / 16777216.0f); /* (0, 1] */
     float c, s;
     orc_sincos_turns(u01(w[1]), &c, &s);
-    float z = sqrtf(-2.0f * logf(u1)) * c;
+    float z = sqrtf(-2.0f * orc_log_unit(u1)) * c;
     float yy = y_center + z * y_sd;
     yy = yy < y_min ? y_min : yy; /* y.clamp(y_min, y_max) (src/main.rs:205) */
     yy = yy > y_max ? y_max : yy;

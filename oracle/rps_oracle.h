@@ -35,6 +35,8 @@ typedef struct orc_stats {
 void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 /* Deterministic polynomial sin/cos of 2*pi*u, u in [0,1). */
 void orc_sincos_turns(float u, float* c, float* s);
+/* Deterministic ln(u), u in (0, 1] normal (initial scatter's Box-Muller). */
+float orc_log_unit(float u);
 /* Attractor k position at time t (double precision, rounded to float). */
 void orc_attractor_pos(const rps_attractor* a, double t, float* px, float* py);
 

@@ -52,12 +52,13 @@ struct rps_ctx {
   f2* pred = nullptr;
   uint32_t P = 0;
   uint32_t sort_passes = 0, sort_launches = 0;
+  uint8_t sph_batch_d = 0, sph_batch_s = 0;  // forced scan batches (0: by size)
   // N-body
   f2* pos_all = nullptr;
   uint64_t ns_padded = 0;
   float *ax = nullptr, *ay = nullptr;
   f2* nb_part = nullptr;  // N-body source-split partials (nb_splits x n float2)
-  uint32_t nb_splits = 0;
+  uint32_t nb_splits = 0;  // source splits of the force launch (RPS_NBODY_SPLITS overrides)
   // device config (pinned upload)
   rps_config* d_cfg = nullptr;
   rps_config* h_cfg_pinned = nullptr;
@@ -275,6 +276,8 @@ SphBuffers sph_buffers(rps_ctx* ctx) {
   b.pred = ctx->pred;
   b.n = (uint32_t)ctx->n;
   b.p = ctx->P;
+  b.batch_d = ctx->sph_batch_d;
+  b.batch_s = ctx->sph_batch_s;
   return b;
 }
 
@@ -502,6 +505,12 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
   ctx->stream_grid = (uint32_t)std::max(0, env_int("RPS_STREAM_GRID", 0));
   ctx->nontemporal = env_int("RPS_STREAM_NT", 3) & 3;  // bit 0 loads, bit 1 stores
   ctx->xcd_order = env_int("RPS_STREAM_XCD", 0) != 0;  // measured slower
+  // Tuning knobs read per context (A/B sweeps, and tests that force a variant at small N).
+  {
+    const int both = env_int("RPS_SPH_BATCH", 0);
+    ctx->sph_batch_d = (uint8_t)std::max(0, std::min(255, env_int("RPS_SPH_BATCH_D", both)));
+    ctx->sph_batch_s = (uint8_t)std::max(0, std::min(255, env_int("RPS_SPH_BATCH_S", both)));
+  }
 
   auto bail = [&](int code) {
     std::string m = ctx->err;
@@ -557,7 +566,9 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     slots.push_back({(void**)&ctx->pos_all, align_up(ctx->ns_padded * sizeof(f2), 256)});
     slots.push_back({(void**)&ctx->ax, nf});
     slots.push_back({(void**)&ctx->ay, nf});
-    ctx->nb_splits = nbody_splits_for(n, ctx->ns_padded);
+    const int forced = env_int("RPS_NBODY_SPLITS", 0);  // > 0: force the split count
+    ctx->nb_splits = forced > 0 ? (uint32_t)std::min<uint64_t>((uint64_t)forced, ctx->ns_padded / kNbodyTile)
+                                : nbody_splits_for(n, ctx->ns_padded);
     if (ctx->nb_splits > 1)
       slots.push_back({(void**)&ctx->nb_part, align_up((size_t)ctx->nb_splits * n * sizeof(f2), 256)});
   }

@@ -213,6 +213,33 @@ __device__ __forceinline__ void sincos_turns(float u, float& c_out, float& s_out
   }
 }
 
+// ln(u) for u in (0, 1] (normal): exponent split by bit operations, then the atanh series
+// ln m = 2 s (1 + s^2/3 + ... + s^14/15), s = (m - 1)/(m + 1), m in [sqrt(1/2), sqrt(2)).
+// Only exact bit operations and fixed-order correctly rounded +, *, / -- bit for bit the
+// oracle's orc_log_unit; within 2 ulp of logf.
+__device__ __forceinline__ float log_unit(float u) {
+  const uint32_t b = __float_as_uint(u);
+  int e = (int)((b >> 23) & 255u) - 127;
+  float m = __uint_as_float((b & 0x007fffffu) | 0x3f800000u);
+  if (m > 1.41421356f) {
+    m = m * 0.5f;
+    e = e + 1;
+  }
+  const float s = (m - 1.0f) / (m + 1.0f);
+  const float s2 = s * s;
+  float p = 6.66666666666666667e-02f;  // 1/15
+  p = p * s2 + 7.69230769230769231e-02f;  // 1/13
+  p = p * s2 + 9.09090909090909091e-02f;  // 1/11
+  p = p * s2 + 1.11111111111111111e-01f;  // 1/9
+  p = p * s2 + 1.42857142857142857e-01f;  // 1/7
+  p = p * s2 + 2.00000000000000000e-01f;  // 1/5
+  p = p * s2 + 3.33333333333333333e-01f;  // 1/3
+  const float t = s + s;
+  const float lnm = t + t * (s2 * p);
+  const float ef = (float)e;
+  return ef * 6.93145751953125e-01f + (ef * 1.42860682030941723e-06f + lnm);
+}
+
 // ---------------------------------------------------------------------------------------
 // Reference helpers
 // ---------------------------------------------------------------------------------------

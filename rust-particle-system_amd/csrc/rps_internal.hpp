@@ -65,13 +65,17 @@ hipError_t launch_init_scatter(const InitArgs& a, hipStream_t s);
 constexpr uint32_t kNbodyTile = 512;  // sources staged per LDS tile (float2: 4 KiB)
 hipError_t launch_nbody_pack(const float* x, const float* y, f2* pos, uint64_t n, hipStream_t s);
 hipError_t launch_nbody_pad(f2* pos, uint64_t from, uint64_t to, hipStream_t s);
-// Source splits: enough workgroups to fill the chip (>= kNbodyMinBlocks) when the targets
-// alone are too few; each split adds nt float2 partials (part holds part_cap of them).
-constexpr uint32_t kNbodyMinBlocks = 2048;
+// Source splits: at least kNbodyMinBlocks workgroups, so the last partial round of resident
+// workgroups (768 at 3 per CU) is a small share of the launch: 2^21 particles 0.785 of FP32
+// peak with 2 splits (2048 workgroups), 0.799 with 12, 0.801 with 24 and 48
+// (tools/ab_nbody.py).  Each split adds nt float2 partials and a fixed-order reduce.
+constexpr uint32_t kNbodyMinBlocks = 24576;
 constexpr uint32_t kNbodyMaxSplits = 64;
 uint32_t nbody_splits_for(uint64_t nt, uint64_t ns_padded);
+// `splits` source splits (1: the kernel writes the accelerations directly; > 1: each split
+// writes nt float2 partials into `part` and a fixed-order reduce follows).
 hipError_t launch_nbody_accel(const f2* pos, uint64_t ns_padded, uint64_t t0, uint64_t nt,
-                              float eps2, float gm, f2* part, uint32_t part_cap, float* ax,
+                              float eps2, float gm, f2* part, uint32_t splits, float* ax,
                               float* ay, hipStream_t s);
 struct NbodyIntegrateArgs {
   float* x;
@@ -111,7 +115,11 @@ struct SphBuffers {
   SphSlots sl;
   uint32_t n;        // N
   uint32_t p;        // next_pow2(N)
+  uint8_t batch_d;   // scan entries in flight per lane, density / sim pass (4, 8, 16;
+  uint8_t batch_s;   //   0: by size, sph_batch); per context, RPS_SPH_BATCH[_D|_S] at create
 };
+// Scan batch of the density (`density`) or sim pass at P entries; `forced` != 0 wins.
+int sph_batch(bool density, uint32_t p, int forced);
 // Runs the whole bitonic network of src/particle_compute.rs:117-149; returns the number of
 // reference passes covered (S(S+1)/2) in *passes.
 hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,

@@ -526,7 +526,7 @@ __global__ __launch_bounds__(kBlock) void init_scatter_kernel(InitArgs a) {
   const float u1 = (float)((w[0] >> 8) + 1u) * (1.0f / 16777216.0f);
   float c, s;
   sincos_turns(u01(w[1]), c, s);
-  const float z = sqrtf(-2.0f * logf(u1)) * c;
+  const float z = sqrtf(-2.0f * log_unit(u1)) * c;
   const float y_center = (a.y_min + a.y_max) / 2.0f;
   const float y_sd = (a.y_max - a.y_min) * 0.125f;
   float yy = y_center + z * y_sd;
@@ -539,134 +539,6 @@ __global__ __launch_bounds__(kBlock) void init_scatter_kernel(InitArgs a) {
     a.f.exp[lidx(a.exp_layout, i)] =
         (uint16_t)(a.clock + life_steps(a.life_min + u01(w[2]) * a.life_range, a.dt) - 1u);
   }
-}
-
-// ---------------------------------------------------------------------------------------
-// All-pairs N-body: float2 source tiles staged through LDS, 4 targets per lane in
-// registers, v_rsq_f32 + FMA inner loop.  FP32-VALU bound.
-// ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void nbody_pack_kernel(const float* x, const float* y,
-                                                            f2* pos, uint64_t n) {
-  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i < n) pos[i] = f2{x[i], y[i]};
-}
-
-__global__ __launch_bounds__(kBlock) void nbody_pad_kernel(f2* pos, uint64_t from, uint64_t to) {
-  const uint64_t i = from + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  // Far-away padding: r2 = 2e36 -> inv^3 underflows to 0, so a pad adds exactly +0.
-  if (i < to) pos[i] = f2{1.0e18f, 1.0e18f};
-}
-
-constexpr int kTargetsPerLane = 8;
-constexpr int kTargetPairs = kTargetsPerLane / 2;
-
-// Each lane owns kTargetsPerLane targets as kTargetPairs float2 pairs (targets t and
-// t + kBlock in one pair), so every operation of the interaction except the rsq is one
-// v_pk_* instruction covering two targets: per 2 interactions 8 packed ops + 2 v_rsq_f32
-// (the FP32-VALU issue floor for this formula).  Per target the arithmetic
-// is the scalar formula r2 = dx*dx + (dy*dy + eps2) with explicit FMAs, unchanged.
-//
-// Source split (blockIdx.y): when the targets alone give too few workgroups to fill 256 CUs
-// (small N, or a strong-scaled shard), the sources are cut into gridDim.y contiguous ranges
-// of whole LDS tiles; each workgroup writes its raw partial sums to part[split][target] and
-// nbody_reduce_kernel adds them in split order (deterministic, no atomics).
-__global__ __launch_bounds__(kBlock) void nbody_accel_kernel(const f2* __restrict__ pos,
-                                                             uint64_t ns_padded, uint64_t t0,
-                                                             uint64_t nt, float eps2, float gm,
-                                                             uint64_t split_len,
-                                                             f2* __restrict__ part,
-                                                             float* __restrict__ ax_out,
-                                                             float* __restrict__ ay_out) {
-  __shared__ f4 tile[kNbodyTile / 2];  // pairs of float2 sources
-  const uint64_t base = (uint64_t)blockIdx.x * kBlock * kTargetsPerLane;
-  f2 tx[kTargetPairs], ty[kTargetPairs], ax[kTargetPairs], ay[kTargetPairs];
-#pragma unroll
-  for (int p = 0; p < kTargetPairs; ++p) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const uint64_t t = base + threadIdx.x + (uint64_t)(2 * p + h) * kBlock;
-      const f2 q = t < nt ? pos[t0 + t] : f2{0.0f, 0.0f};
-      tx[p][h] = q[0];
-      ty[p][h] = q[1];
-    }
-    ax[p] = f2{0.0f, 0.0f};
-    ay[p] = f2{0.0f, 0.0f};
-  }
-  const f2 e2 = {eps2, eps2};
-  const f4* src4 = reinterpret_cast<const f4*>(pos);
-  const uint64_t s_begin = (uint64_t)blockIdx.y * split_len;
-  const uint64_t s_end = s_begin + split_len < ns_padded ? s_begin + split_len : ns_padded;
-  for (uint64_t s0 = s_begin; s0 < s_end; s0 += kNbodyTile) {
-    __syncthreads();
-    for (uint32_t q = threadIdx.x; q < kNbodyTile / 2; q += kBlock) tile[q] = src4[(s0 >> 1) + q];
-    __syncthreads();
-#pragma unroll 2
-    for (uint32_t q = 0; q < kNbodyTile / 2; ++q) {
-      const f4 sp = tile[q];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const f2 sx = {sp[2 * h], sp[2 * h]}, sy = {sp[2 * h + 1], sp[2 * h + 1]};
-#pragma unroll
-        for (int p = 0; p < kTargetPairs; ++p) {
-          const f2 dx = sx - tx[p];
-          const f2 dy = sy - ty[p];
-          const f2 r2 = __builtin_elementwise_fma(dx, dx, __builtin_elementwise_fma(dy, dy, e2));
-          const f2 inv = {__builtin_amdgcn_rsqf(r2[0]), __builtin_amdgcn_rsqf(r2[1])};
-          const f2 inv3 = (inv * inv) * inv;
-          ax[p] = __builtin_elementwise_fma(dx, inv3, ax[p]);
-          ay[p] = __builtin_elementwise_fma(dy, inv3, ay[p]);
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int p = 0; p < kTargetPairs; ++p) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const uint64_t t = base + threadIdx.x + (uint64_t)(2 * p + h) * kBlock;
-      if (t < nt) {
-        if (part) {
-          part[(uint64_t)blockIdx.y * nt + t] = f2{ax[p][h], ay[p][h]};
-        } else {
-          ax_out[t] = ax[p][h] * gm;
-          ay_out[t] = ay[p][h] * gm;
-        }
-      }
-    }
-  }
-}
-
-__global__ __launch_bounds__(kBlock) void nbody_reduce_kernel(const f2* __restrict__ part,
-                                                              uint32_t splits, uint64_t nt,
-                                                              float gm, float* __restrict__ ax_out,
-                                                              float* __restrict__ ay_out) {
-  const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (t >= nt) return;
-  f2 a = part[t];
-  for (uint32_t s = 1; s < splits; ++s) a += part[(uint64_t)s * nt + t];
-  ax_out[t] = a[0] * gm;
-  ay_out[t] = a[1] * gm;
-}
-
-__global__ __launch_bounds__(kBlock) void nbody_integrate_kernel(NbodyIntegrateArgs a) {
-  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= a.n) return;
-  float px = a.x[i], py = a.y[i], qx = a.vx[i], qy = a.vy[i];
-  qx = qx + a.gx_dt;
-  qy = qy + a.gy_dt;
-  qx = qx + a.ax[i] * a.dt;
-  qy = qy + a.ay[i] * a.dt;
-  if (a.drag_on) {
-    qx = qx * a.drag_f;
-    qy = qy * a.drag_f;
-  }
-  px = px + qx * a.dt;
-  py = py + qy * a.dt;
-  wall(a.x_min, a.x_max, a.y_min, a.y_max, a.damping, px, py, qx, qy);
-  a.x[i] = px;
-  a.y[i] = py;
-  a.vx[i] = qx;
-  a.vy[i] = qy;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1413,53 +1285,6 @@ hipError_t launch_init_scatter(const InitArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_nbody_pack(const float* x, const float* y, f2* pos, uint64_t n, hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(nbody_pack_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, s, x, y, pos, n);
-  return hipGetLastError();
-}
-
-hipError_t launch_nbody_pad(f2* pos, uint64_t from, uint64_t to, hipStream_t s) {
-  if (to <= from) return hipSuccess;
-  hipLaunchKernelGGL(nbody_pad_kernel, dim3(blocks_for(to - from)), dim3(kBlock), 0, s, pos, from,
-                     to);
-  return hipGetLastError();
-}
-
-uint32_t nbody_splits_for(uint64_t nt, uint64_t ns_padded) {
-  if (nt == 0) return 1;
-  const uint64_t tb = blocks_for(nt, kBlock * kTargetsPerLane);
-  const uint64_t tiles = ns_padded / kNbodyTile;
-  uint64_t s = (kNbodyMinBlocks + tb - 1) / tb;
-  if (s > kNbodyMaxSplits) s = kNbodyMaxSplits;
-  if (s > tiles) s = tiles;
-  return s < 1 ? 1u : (uint32_t)s;
-}
-
-hipError_t launch_nbody_accel(const f2* pos, uint64_t ns_padded, uint64_t t0, uint64_t nt,
-                              float eps2, float gm, f2* part, uint32_t part_cap, float* ax,
-                              float* ay, hipStream_t s) {
-  if (nt == 0) return hipSuccess;
-  uint32_t splits = nbody_splits_for(nt, ns_padded);
-  if (splits > part_cap) splits = part_cap;
-  const uint64_t tiles = ns_padded / kNbodyTile;
-  const uint64_t split_len = (tiles + splits - 1) / splits * kNbodyTile;
-  splits = (uint32_t)((ns_padded + split_len - 1) / split_len);  // no empty split
-  f2* p = splits > 1 ? part : nullptr;
-  hipLaunchKernelGGL(nbody_accel_kernel, dim3(blocks_for(nt, kBlock * kTargetsPerLane), splits),
-                     dim3(kBlock), 0, s, pos, ns_padded, t0, nt, eps2, gm, split_len, p, ax, ay);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess || !p) return e;
-  hipLaunchKernelGGL(nbody_reduce_kernel, dim3(blocks_for(nt)), dim3(kBlock), 0, s, p, splits, nt, gm,
-                     ax, ay);
-  return hipGetLastError();
-}
-
-hipError_t launch_nbody_integrate(const NbodyIntegrateArgs& a, hipStream_t s) {
-  if (a.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(nbody_integrate_kernel, dim3(blocks_for(a.n)), dim3(kBlock), 0, s, a);
-  return hipGetLastError();
-}
 
 
 // Launch K global passes of one stage starting at stride G (flip = it is the stage's first).
@@ -1594,20 +1419,11 @@ hipError_t launch_sph_offsets(const SphBuffers& b, hipStream_t s) {
   return hipGetLastError();
 }
 
-// Entries in flight per lane in the density (`d`) and sim scans: RPS_SPH_BATCH_D /
-// RPS_SPH_BATCH_S, else RPS_SPH_BATCH, else by size (measured).
-static int sph_env_batch(const char* name) {
-  const char* v = std::getenv(name);
-  const int k = v && *v ? std::atoi(v) : 0;
-  return k == 4 || k == 8 || k == 16 ? k : 0;
-}
-static int sph_batch(bool density, uint32_t p) {
-  static const int both = sph_env_batch("RPS_SPH_BATCH");
-  static const int d = sph_env_batch("RPS_SPH_BATCH_D");
-  static const int sim = sph_env_batch("RPS_SPH_BATCH_S");
-  const int k = density ? d : sim;
-  if (k) return k;
-  if (both) return both;
+// Entries in flight per lane in the density and sim scans, unless the context forces one
+// (SphBuffers::batch_d / batch_s, from RPS_SPH_BATCH[_D|_S] at rps_create): by size, measured
+// (DESIGN.md §5).
+int sph_batch(bool density, uint32_t p, int forced) {
+  if (forced == 4 || forced == 8 || forced == 16) return forced;
   // The sim scan keeps 4 entries in flight up to P = 2^21, where its slot records stay in
   // the caches (2^20 frame 0.404 -> 0.392 ms, 2^21 0.670 -> 0.651), and 8 beyond (2^22: 1.25
   // vs 1.28 ms with 4).  The density scan is indifferent (4 or 8 within 0.3 %).
@@ -1630,7 +1446,7 @@ hipError_t launch_sph_pre(const SphBuffers& b, hipStream_t s, bool with_offsets)
 #define RPS_DENSITY(B)                                                                           \
   hipLaunchKernelGGL(sph_density_kernel<B>, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg, \
                      b.offsets, b.ends, b.sl, b.p)
-  switch (sph_batch(true, b.p)) {
+  switch (sph_batch(true, b.p, b.batch_d)) {
     case 4: RPS_DENSITY(4); break;
     case 16: RPS_DENSITY(16); break;
     default: RPS_DENSITY(8); break;
@@ -1647,7 +1463,7 @@ hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s) {
   else                                                                                         \
     hipLaunchKernelGGL((sph_sim_kernel<B, true>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s,   \
                        b.cfg, b.offsets, b.ends, b.sl, b.st2, b.p)
-  switch (sph_batch(false, b.p)) {
+  switch (sph_batch(false, b.p, b.batch_s)) {
     case 4: RPS_SIM(4); break;
     case 16: RPS_SIM(16); break;
     default: RPS_SIM(8); break;

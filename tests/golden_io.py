@@ -4,7 +4,7 @@ import os
 import numpy as np
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-STREAM = ("stream_c1_subset.npz", "stream_c2_verlet.npz", "stream_c3_features.npz")
+STREAM = ("stream_c1_subset.npz", "stream_c1_attractor.npz", "stream_c2_verlet.npz", "stream_c3_features.npz")
 SPH = ("sph_n1000.npz", "sph_n2048.npz")
 NBODY = ("nbody_n1024.npz",)
 
@@ -19,6 +19,16 @@ def structs(rps, g):
     cfg = rps.ParticleConfig.from_buffer_copy(g["cfg"].tobytes())
     ext = rps.ExtConfig.from_buffer_copy(g["ext"].tobytes())
     return cfg, ext
+
+
+def active_steps(g, ext):
+    """(frame, active-step index) of the fixture's active frames: rps_step advances
+    frame_count first and runs a step once frame_count >= shader_delay (wgsl:426)."""
+    out = []
+    for f in range(1, int(g["steps"][0]) + 1):
+        if f >= ext.shader_delay:
+            out.append((f, len(out)))
+    return out
 
 
 def inputs(g):

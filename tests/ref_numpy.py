@@ -62,6 +62,53 @@ def sincos_turns(u):
     return co.astype(F), so.astype(F)
 
 
+LOG_C = [F(1 / 15), F(1 / 13), F(1 / 11), F(1 / 9), F(1 / 7), F(1 / 5), F(1 / 3)]
+
+
+def log_unit(u):
+    """ln(u), u in (0, 1]: exponent split by bit operations + the atanh series (the oracle's
+    orc_log_unit, the device's log_unit)."""
+    u = np.asarray(u, F)
+    b = u.view(np.uint32)
+    e = ((b >> np.uint32(23)) & np.uint32(255)).astype(np.int32) - 127
+    m = ((b & np.uint32(0x007FFFFF)) | np.uint32(0x3F800000)).view(F)
+    big = m > F(1.41421356)
+    m = np.where(big, m * F(0.5), m).astype(F)
+    e = np.where(big, e + 1, e)
+    s = (m - F(1.0)) / (m + F(1.0))
+    s2 = s * s
+    p = np.full_like(s2, LOG_C[0])
+    for c in LOG_C[1:]:
+        p = p * s2 + c
+    t = s + s
+    lnm = t + t * (s2 * p)
+    ef = e.astype(F)
+    return (ef * F(6.93145751953125e-01) + (ef * F(1.42860682030941723e-06) + lnm)).astype(F)
+
+
+def init_scatter(bounds, seed, n, id_offset=0, global_count=None):
+    """x, y of the seeded initial scatter (src/main.rs:191-205; the oracle's orc_init_scatter):
+    x linear in the global id, y = Box-Muller normal from Philox with the fixed-op log."""
+    global_count = global_count or (id_offset + n)
+    x_min, x_max, y_min, y_max = (F(v) for v in bounds)
+    g = np.arange(id_offset, id_offset + n, dtype=np.uint64)
+    t = g.astype(F) / F(global_count)
+    x = x_min + t * (x_max - x_min)
+    k0, k1 = seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF
+    ones = np.full(n, 0xFFFFFFFF, np.uint32)
+    w = philox4x32_10(g.astype(np.uint32), (g >> np.uint64(32)).astype(np.uint32), ones, ones, k0, k1)
+    u1 = ((np.asarray(w[0], np.uint32) >> np.uint32(8)) + np.uint32(1)).astype(F) * F(1.0 / 16777216.0)
+    c, _ = sincos_turns(u01(w[1]))
+    with np.errstate(invalid="ignore"):
+        z = np.sqrt(F(-2.0) * log_unit(u1)) * c
+    yc = (y_min + y_max) / F(2.0)
+    sd = (y_max - y_min) * F(0.125)
+    y = yc + z * sd
+    y = np.where(y < y_min, y_min, y)
+    y = np.where(y > y_max, y_max, y).astype(F)
+    return x.astype(F), y
+
+
 def attractor_positions(ext, active_step):
     dt = float(F(ext["dt"]))
     t = float(active_step) * dt

@@ -138,3 +138,79 @@ def test_nbody_sharded_external_exchange(gpu, orc):
     finally:
         for c in ctxs:
             c.close()
+
+
+@pytest.mark.parametrize("splits", [1, 2, 7])
+def test_nbody_forced_split_variants(gpu, orc, monkeypatch, splits):
+    """Both branches of the force launch at a small N: one source split (the kernel writes
+    G*a directly, the variant every launch with >= 2048 target blocks runs, e.g. the bench's
+    2^22 and the C4 2^24 step) and several splits (partials + the fixed-order reduce),
+    forced per context with RPS_NBODY_SPLITS."""
+    rps = gpu
+    monkeypatch.setenv("RPS_NBODY_SPLITS", str(splits))
+    n = 6000
+    cfg = config_c1(rps, n)
+    ext = rps.make_ext(nbody_strength=30.0, nbody_softening=1.0, shader_delay=0)
+    g = np.random.default_rng(100 + splits)
+    soa = dict(x=g.uniform(-900, 900, n).astype(F), y=g.uniform(-500, 500, n).astype(F),
+               vx=np.zeros(n, F), vy=np.zeros(n, F))
+    with rps.Context(n, rps.MODE_NBODY) as ctx:
+        ctx.set_config(cfg, ext)
+        ctx.upload_soa(soa)
+        ctx.step(1)
+        ax = ctx.read_debug(rps.DEBUG_ACCEL_X)
+        ay = ctx.read_debug(rps.DEBUG_ACCEL_Y)
+    rx, ry = orc.nbody_accel(ext, soa["x"], soa["y"])
+    _check_accel(ax, ay, rx, ry, ext, soa["x"], soa["y"])
+
+
+def _abs_sum_targets(ext, tx, ty, sx, sy):
+    """sum_j |f_ij| for a few targets over all sources (f64, one target at a time)."""
+    sx64, sy64 = sx.astype(np.float64), sy.astype(np.float64)
+    e2 = float(ext.nbody_softening) ** 2
+    out = np.zeros(len(tx))
+    for i in range(len(tx)):
+        dx = sx64 - float(tx[i])
+        dy = sy64 - float(ty[i])
+        d2 = dx * dx + dy * dy
+        out[i] = (np.sqrt(d2) * (d2 + e2) ** -1.5).sum()
+    return out * float(ext.nbody_strength)
+
+
+@pytest.mark.parametrize("splits", [None, "1"])
+def test_nbody_full_size(gpu, orc, monkeypatch, splits):
+    """2^22 targets over 2^22 sources -- the bench's `allpairs` step: the default source
+    splits (12 at this size) and one forced split (the kernel writes G*a directly, the
+    variant launches with >= 24576 target blocks run).  Four chunks of 16 contiguous
+    targets spread over the array (first block, middle, the last block's tail) are checked
+    against the oracle's f64 direct sum over every source, with the same bound as the small
+    tests (the two-level summation keeps the error near 1e-6 of |a| at this size); the
+    integration of every particle given the device accelerations is bitwise."""
+    if splits:
+        monkeypatch.setenv("RPS_NBODY_SPLITS", splits)
+    rps = gpu
+    n = 1 << 22
+    cfg = config_c1(rps, n)
+    ext = rps.make_ext(nbody_strength=1.0e3, nbody_softening=1.0, shader_delay=0)
+    g = np.random.default_rng(2024)
+    soa = dict(x=g.uniform(-950, 950, n).astype(F), y=g.uniform(-530, 530, n).astype(F),
+               vx=g.normal(0, 10, n).astype(F), vy=g.normal(0, 10, n).astype(F))
+    with rps.Context(n, rps.MODE_NBODY) as ctx:
+        ctx.set_config(cfg, ext)
+        ctx.upload_soa(soa)
+        ctx.step(1)
+        ax = ctx.read_debug(rps.DEBUG_ACCEL_X)
+        ay = ctx.read_debug(rps.DEBUG_ACCEL_Y)
+        got = ctx.download_soa()
+    for t0 in (0, 2048 * 8 + 5, n // 2 + 123, n - 16):
+        rx, ry = orc.nbody_accel(ext, soa["x"], soa["y"], t0=t0, nt=16)
+        gx, gy = ax[t0:t0 + 16], ay[t0:t0 + 16]
+        mag = np.hypot(rx.astype(np.float64), ry.astype(np.float64))
+        err = np.hypot(gx.astype(np.float64) - rx, gy.astype(np.float64) - ry)
+        bound = np.maximum(1e-4 * mag, 1e-5 * _abs_sum_targets(ext, soa["x"][t0:t0 + 16], soa["y"][t0:t0 + 16],
+                                                               soa["x"], soa["y"]))
+        assert np.max(err / bound) <= 1.0, (t0, np.max(err / bound))
+        assert np.median(err / mag) < 1e-5, (t0, np.median(err / mag))
+    ref = copy_soa(soa)
+    orc.nbody_integrate(cfg, ext, ax, ay, ref)
+    assert_soa_bitwise(got, ref)

@@ -153,3 +153,31 @@ def test_sph_large_frames_bitwise(gpu, orc, n):
     rps = gpu
     cfg = rps.default_particle_config(n, gravity=100.0)
     _frames_vs_oracle(rps, orc, n, _blob(n, 3, spread=260.0), cfg, 2)
+
+
+@pytest.mark.parametrize("n", [65536, 50000])
+@pytest.mark.parametrize("batch", [("RPS_SPH_BATCH_S", "8"), ("RPS_SPH_BATCH_S", "16"),
+                                   ("RPS_SPH_BATCH_D", "4"), ("RPS_SPH_BATCH_D", "16")])
+def test_sph_forced_scan_batches(gpu, orc, monkeypatch, n, batch):
+    """Every scan-batch variant of the density and sim kernels, forced per context at small N
+    (the default picks the sim batch 8 only above P = 2^21): P = N (slot self-skip) and
+    N = 50 000 (pads, index self-skip), every pass bitwise over 3 frames."""
+    rps = gpu
+    monkeypatch.setenv(*batch)
+    cfg = rps.default_particle_config(n, gravity=100.0)
+    _frames_vs_oracle(rps, orc, n, _blob(n, n + 2), cfg, 3)
+
+
+def test_sph_bench_workload_full_size(gpu, orc):
+    """The bench's `sph` workload exactly: 2^22 particles of the reference scatter over a
+    viewport scaled to the default density, every frame active.  P > 2^21 selects the sim
+    scan's 8-entry batch and 8192-entry sort tiles with 3 passes per register chunk; two
+    frames, every pass bitwise."""
+    rps = gpu
+    n = 1 << 22
+    scale = (n / 50000) ** 0.5
+    cfg = rps.default_particle_config(n, screen_bounds=rps.screen_bounds_for(1920.0 * scale, 1080.0 * scale))
+    parts = rps.setup_particles_scatter(cfg, n, seed=0x5EED)
+    soa = dict(x=parts["position"][:, 0].copy(), y=parts["position"][:, 1].copy(),
+               vx=parts["velocity"][:, 0].copy(), vy=parts["velocity"][:, 1].copy())
+    _frames_vs_oracle(rps, orc, n, soa, cfg, 2)

@@ -5,8 +5,8 @@ both compute IEEE f32 with no contraction and correctly-rounded div/sqrt (DESIGN
 import numpy as np
 import pytest
 
-from helpers import (F, assert_bitwise, assert_soa_bitwise, config_c1, copy_soa, ext_verlet_1att,
-                     random_soa, soa_to_particles)
+from helpers import (F, assert_bitwise, assert_soa_bitwise, config_c1, copy_soa, ext_c1_attractor,
+                     ext_verlet_1att, random_soa, soa_to_particles)
 
 pytestmark = pytest.mark.gpu
 
@@ -53,6 +53,33 @@ def test_c1_reference_subset_with_shader_delay(gpu, orc):
         aos = ctx.download()
         want_c = orc.set_color_array(soa["vx"], soa["vy"], cfg.max_energy)
         assert_bitwise(aos["color"].reshape(-1), want_c.reshape(-1), "colour")
+
+
+def test_c1_single_attractor_euler_baseline_config(gpu, orc):
+    """C1 exactly as BASELINE.json configs[0] states it: 65 536 particles of the reference
+    scatter, a single point attractor at the origin, semi-implicit Euler, SHADER_DELAY 5
+    (4 gated frames, then active steps; compute_shader.wgsl:392-400, :69-99, :426)."""
+    rps = gpu
+    n = 65536
+    cfg = config_c1(rps, n, gravity=9.8)
+    ext = ext_c1_attractor(rps)
+    ext.shader_delay = 5
+    parts = rps.setup_particles_scatter(cfg, n, seed=7)
+    soa = dict(x=parts["position"][:, 0].copy(), y=parts["position"][:, 1].copy(),
+               vx=parts["velocity"][:, 0].copy(), vy=parts["velocity"][:, 1].copy())
+    with rps.Context(n) as ctx:
+        ctx.set_config(cfg, ext)
+        ctx.upload(parts)
+        fc, act = 0, 0
+        for chunk in (4, 1, 7, 48):
+            ctx.step(chunk)
+            fc, act = orc.run_steps(0, cfg, ext, soa, chunk, frame_count=fc, active_steps=act)
+            assert ctx.counters() == (fc, act)
+            assert_soa_bitwise(ctx.download_soa(), soa, what=f"frame{fc} ")
+        assert (fc, act) == (60, 56)
+        aos = ctx.download()
+    want_c = orc.set_color_array(soa["vx"], soa["vy"], cfg.max_energy)
+    assert_bitwise(aos["color"].reshape(-1), want_c.reshape(-1), "colour")
 
 
 def test_c2_verlet_one_attractor(gpu, orc):
@@ -154,10 +181,9 @@ def test_init_scatter_matches_oracle(gpu, orc):
         ctx.init_scatter(seed=99)
         got = ctx.download_soa(life=True)
     want = orc.init_scatter(cfg, ext, 99, n, id_offset=5000, global_count=200000)
-    for k in ("x", "vx", "vy", "life"):
+    # Bitwise, y included: the Box-Muller ln is the fixed-op log_unit on both sides.
+    for k in ("x", "y", "vx", "vy", "life"):
         assert_bitwise(got[k], want[k], k)
-    # y goes through logf (device ocml vs glibc): allow 1 ulp-level differences.
-    np.testing.assert_allclose(got["y"], want["y"], rtol=0, atol=1e-3)
     assert (got["y"] >= cfg.screen_bounds[2]).all() and (got["y"] <= cfg.screen_bounds[3]).all()
 
 

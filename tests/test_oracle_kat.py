@@ -130,3 +130,36 @@ def test_life_steps_kat(orc):
     assert orc.life_steps(0.005, dt) == 1
     assert orc.life_steps(1.0, dt) == int(np.ceil(np.float32(1.0) / dt))
     assert orc.life_steps(5.0, dt) == int(np.ceil(np.float32(5.0) / dt))
+
+
+def test_log_unit_accuracy_and_restatement(orc):
+    """The initial scatter's fixed-op ln (orc_log_unit; device log_unit): within 2 ulp of the
+    exact ln over every Box-Muller input u = k/2^24, k = 1..2^24, and the numpy restatement
+    equals the C oracle bit for bit on a sample (incl. both ends and the sqrt(2) split)."""
+    k = np.arange(1, (1 << 24) + 1, dtype=np.float64)
+    u = (k / 16777216.0).astype(F)
+    got = RN.log_unit(u)
+    exact = np.log(u.astype(np.float64))
+    ulp = np.spacing(np.abs(exact).astype(F)).astype(np.float64)
+    nz = u != F(1.0)
+    assert np.max(np.abs(got[nz].astype(np.float64) - exact[nz]) / ulp[nz]) <= 2.0
+    assert got[-1] == F(0.0)
+    g = np.random.default_rng(4)
+    idx = np.concatenate([[0, 1, 2, (1 << 24) - 1], g.integers(0, 1 << 24, 20000)])
+    m = np.float32(1.41421356)
+    edge = np.array([m, np.nextafter(m, F(2)), np.nextafter(m, F(0))], F) * F(0.25)
+    for v in np.concatenate([u[idx], edge]):
+        assert f32_bits(orc.log_unit(float(v))) == f32_bits(RN.log_unit(np.array([v], F))[0]), v
+
+
+def test_init_scatter_matches_numpy(rps, orc):
+    """orc_init_scatter's x and y (Philox + sincos_turns + log_unit Box-Muller, clamped) equal
+    the numpy restatement bit for bit, on a shard with a 64-bit id offset."""
+    cfg = rps.default_particle_config(50000)
+    ext = rps.headline_ext()
+    for off, total in ((0, 50000), ((1 << 33) + 7, 1 << 34)):
+        soa = orc.init_scatter(cfg, ext, 0xABCDEF0123, 50000, id_offset=off, global_count=total)
+        x, y = RN.init_scatter(list(cfg.screen_bounds), 0xABCDEF0123, 50000, id_offset=off, global_count=total)
+        assert np.array_equal(soa["x"].view(np.uint32), x.view(np.uint32))
+        assert np.array_equal(soa["y"].view(np.uint32), y.view(np.uint32))
+        assert (y > cfg.screen_bounds[2]).mean() > 0.99
