@@ -31,6 +31,7 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 METRIC = "particle-updates/sec + achieved HBM GB/s, 10^8 particles, 1/2/4/8 MI355X"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+L2_PEAK_GBPS = 34500.0  # MI355X_MICROARCH.md §L2: aggregate over the 8 XCDs, ~34.5 TB/s
 # SURVEY.md §8(d) / BASELINE.md, C3: the algorithmic cost of a particle-step is 40 B (read and
 # write x, y, vx, vy and an f32 lifetime).  The kernel moves 32.03 of them (the lifetime is a u16
 # expiry read and written only in the group-steps where one is due, found from a u16 per group
@@ -59,8 +60,8 @@ def parse():
     ap.add_argument("--sph-n", type=int, default=1 << 22,
                     help="particles of the SPH-frame side measurement per rank (0: skip)")
     ap.add_argument("--sph-frames", type=int, default=50)
-    ap.add_argument("--sph-cpu-n", type=int, default=1 << 20,
-                    help="particles of the SPH CPU-baseline sample (oracle, one thread)")
+    ap.add_argument("--sph-cpu-n", type=int, default=1 << 22,
+                    help="particles of the SPH CPU-baseline sample (oracle, OpenMP)")
     ap.add_argument("--sph-cpu-frames", type=int, default=3)
     ap.add_argument("--allpairs-timeout", type=float, default=240.0,
                     help="watchdog: print the headline line and exit non-zero if a side run hangs")
@@ -278,12 +279,24 @@ def sph_side(rps, args, d):
         d.barrier()
         el = d.max(t1 - t0)
         sim_ms, _ = ctx.kernel_time()
+        cost = ctx.sph_frame_cost()  # algorithmic bytes of the last frame (include/rps.h)
     finally:
         ctx.close()
+    sim_ms = d.max(sim_ms)
+    frame_ms = el * 1e3 / args.sph_frames
+    sim_gbps = cost["sim_bytes"] / (sim_ms * 1e-3) / 1e9
     out = {"workload": f"SPH frame (5 passes, bitwise == oracle), {n} particles per rank, reference scatter",
-           "scaling": "replicas", "frames": args.sph_frames, "ms_per_frame": el * 1e3 / args.sph_frames,
+           "scaling": "replicas", "frames": args.sph_frames, "ms_per_frame": frame_ms,
            "particle_steps_per_s": float(n) * d.world * args.sph_frames / el,
-           "sim_kernel_ms": d.max(sim_ms)}
+           "sim_kernel_ms": sim_ms,
+           "roofline": {"bound": "l2", "kernel": "sph_sim_kernel", "achieved": sim_gbps, "peak": L2_PEAK_GBPS,
+                        "unit": "GB/s", "frac": sim_gbps / L2_PEAK_GBPS, "traffic": None,
+                        "algorithmic_bytes_per_launch": cost["sim_bytes"],
+                        "scanned_entries_per_particle": cost["scanned_entries"] / cost["slots"],
+                        "within_radius_per_particle": cost["within_entries"] / cost["slots"]},
+           "frame_cost": {"bytes": cost["frame_bytes"], "gbps": cost["frame_bytes"] / (frame_ms * 1e-3) / 1e9,
+                          "frac_of_l2": cost["frame_bytes"] / (frame_ms * 1e-3) / 1e9 / L2_PEAK_GBPS,
+                          "sort_launches": cost["sort_launches"]}}
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline and args.sph_cpu_n > 0:
         out["cpu_baseline"] = sph_cpu_baseline(rps, args)
     return out
@@ -291,25 +304,28 @@ def sph_side(rps, args, d):
 
 def sph_cpu_baseline(rps, args):
     """The reference's SPH frame on the host: the oracle's restatement of the five WGSL passes
-    (oracle/rps_oracle.c, one thread) over a bounded sample of the same workload (the
-    reference scatter at the default density), timed after one warm frame."""
+    (oracle/rps_oracle.c, the OpenMP build at the stream baseline's thread count; results
+    identical to the serial checker) over a bounded sample of the same workload (the reference
+    scatter at the default density), timed after one warm frame."""
     import oracle as orc
 
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     n = args.sph_cpu_n
     scale = max(1.0, (n / 50000) ** 0.5)
     cfg = rps.default_particle_config(n, screen_bounds=rps.screen_bounds_for(1920.0 * scale, 1080.0 * scale))
     parts = rps.setup_particles_scatter(cfg, n, seed=args.seed)
     soa = dict(x=parts["position"][:, 0].copy(), y=parts["position"][:, 1].copy(),
                vx=parts["velocity"][:, 0].copy(), vy=parts["velocity"][:, 1].copy())
-    st = orc.SphState(n)
+    st = orc.SphState(n, omp=True, threads=threads)
     ext = rps.make_ext(shader_delay=0)
     fc, _ = orc.run_steps(2, cfg, ext, soa, 1, sph=st)  # warm frame
     t0 = time.perf_counter()
     orc.run_steps(2, cfg, ext, soa, args.sph_cpu_frames, frame_count=fc, sph=st)
     el = time.perf_counter() - t0
-    return {"value": float(n) * args.sph_cpu_frames / el, "unit": "particle-steps/s", "cores": 1, "kind": "port",
+    return {"value": float(n) * args.sph_cpu_frames / el, "unit": "particle-steps/s", "cores": threads,
+            "kind": "port",
             "sample": f"{n} particles x {args.sph_cpu_frames} frames of the five passes (oracle/rps_oracle.c, "
-                      f"one thread), {el:.1f} s; {el * 1e3 / args.sph_cpu_frames:.0f} ms/frame"}
+                      f"-O3 -fopenmp, {threads} threads), {el:.1f} s; {el * 1e3 / args.sph_cpu_frames:.0f} ms/frame"}
 
 
 def stats_check(d, st_all, st_shard):

@@ -264,8 +264,31 @@ int rps_time_steps(rps_ctx* ctx, uint32_t nsteps, double* total_ms);
 void* rps_get_stream(rps_ctx* ctx);
 
 /* Algorithmic HBM bytes (stream/SPH) or flops (N-body) one step moves for this context's
- * mode/config; `unit` receives 0 for bytes, 1 for flops. */
+ * mode/config; `unit` receives 0 for bytes, 1 for flops.  SPH: the frame's
+ * bytes of rps_sph_frame_cost (counts the current state's neighbour entries, blocks). */
 int rps_step_cost(const rps_ctx* ctx, double* amount, int* unit);
+
+/* SPH frame cost, for rooflines: the algorithmic bytes of one active frame
+ * of the current state.  E = neighbour entries the reference's scans visit (the nine runs of
+ * every lookup slot's particle, wgsl:207-254 / :279-384), counted on the device; per kernel:
+ *   sort     launches x P x 16 B (each launch reads and writes the 8-B lookup) + N x 8 B bin
+ *   predict  P x 60 B (lookup, gathered state, slot records) + N x 8 B (offsets, ends)
+ *   density  E x 8 B (neighbour predicted position) + P x 120 B (runs, own record, outputs)
+ *   sim      E x 32 B (pressure {pos, P/rho^2, Pn/(rho rho_n)} + viscosity {pos, v} records)
+ *            + P x 156 B (runs, masks, own records, state write)
+ * The scans' neighbour records are re-read E/P times per frame and served by the caches, so
+ * their roofline is the aggregate L2 bandwidth, not HBM.  Counts the most recent active
+ * frame's runs (RPS_ERR_UNSUPPORTED before one): launches a counting kernel on the context
+ * stream and waits for it (not for timed regions).  SPH mode only. */
+typedef struct rps_sph_cost {
+  uint64_t slots;            /* P = next_pow2(N) */
+  uint64_t particles;        /* N */
+  uint64_t scanned_entries;  /* E */
+  uint64_t within_entries;   /* of E, within the smoothing radius (self included) */
+  uint64_t sort_launches;
+  double sort_bytes, predict_bytes, density_bytes, sim_bytes, frame_bytes;
+} rps_sph_cost;
+int rps_sph_frame_cost(rps_ctx* ctx, rps_sph_cost* out);
 
 /* Multi-GPU: RCCL communicator over this rank's context.  N-body needs it (all-gather of
  * positions); STREAM uses it only for the all-rank stats (rps_get_stats).

@@ -40,6 +40,7 @@ def lib(omp: bool = False) -> ctypes.CDLL:
         "orc_philox4x32_10": (None, [_P, _P, _P]),
         "orc_sincos_turns": (None, [_F, ctypes.POINTER(_F), ctypes.POINTER(_F)]),
         "orc_log_unit": (_F, [_F]),
+        "orc_set_threads": (None, [_I]),
         "orc_attractor_pos": (None, [_P, ctypes.c_double, ctypes.POINTER(_F), ctypes.POINTER(_F)]),
         "orc_set_color": (None, [_F, _F, _F, _P]),
         "orc_hash_cell": (_U32, [ctypes.c_int32, ctypes.c_int32]),
@@ -216,9 +217,10 @@ def nbody_integrate(cfg, ext, ax, ay, soa):
 
 
 class SphState:
-    """Host buffers of the reference's SPH path (src/particle_buffers.rs:84-168)."""
+    """Host buffers of the reference's SPH path (src/particle_buffers.rs:84-168).
+    omp=True runs the passes on the OpenMP build (bench.py's cpu_baseline; same results)."""
 
-    def __init__(self, n):
+    def __init__(self, n, omp=False, threads=0):
         self.n = n
         p = 1
         while p < n:
@@ -228,21 +230,24 @@ class SphState:
         self.offsets = np.zeros(n, np.uint32)
         self.dens = np.zeros(2 * n, np.float32)
         self.pred = np.zeros(2 * n, np.float32)
+        self.omp = omp
+        if omp and threads:
+            lib(omp=True).orc_set_threads(threads)
 
     def grid(self, cfg, soa):
-        L = lib()
+        L = lib(omp=self.omp)
         L.orc_sph_bin(_ref(cfg), _p(soa["x"]), _p(soa["y"]), _p(self.lookup), _p(self.offsets), self.n)
         passes = L.orc_sph_sort(_p(self.lookup), self.n)
         L.orc_sph_offsets(_p(self.lookup), _p(self.offsets), self.n)
         return passes
 
     def pre(self, cfg, soa):
-        lib().orc_sph_pre(_ref(cfg), _p(soa["vx"]), _p(soa["vy"]), _p(soa["x"]), _p(soa["y"]),
-                          _p(self.lookup), _p(self.offsets), _p(self.dens), _p(self.pred), self.n)
+        lib(omp=self.omp).orc_sph_pre(_ref(cfg), _p(soa["vx"]), _p(soa["vy"]), _p(soa["x"]), _p(soa["y"]),
+                                      _p(self.lookup), _p(self.offsets), _p(self.dens), _p(self.pred), self.n)
 
     def sim(self, cfg, soa):
-        lib().orc_sph_sim(_ref(cfg), _p(soa["x"]), _p(soa["y"]), _p(soa["vx"]), _p(soa["vy"]),
-                          _p(self.lookup), _p(self.offsets), _p(self.dens), _p(self.pred), self.n)
+        lib(omp=self.omp).orc_sph_sim(_ref(cfg), _p(soa["x"]), _p(soa["y"]), _p(soa["vx"]), _p(soa["vy"]),
+                                      _p(self.lookup), _p(self.offsets), _p(self.dens), _p(self.pred), self.n)
 
 
 def run_steps(mode, cfg, ext, soa, nsteps, frame_count=0, active_steps=0, id_offset=0, sph=None):

@@ -429,6 +429,15 @@ void orc_stream_step_omp(const rps_config* cfg, const rps_ext_config* ext, uint6
   (void)threads;
 }
 
+/* Thread count of the OpenMP build's parallel loops (no-op in the serial checker). */
+void orc_set_threads(int threads) {
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#else
+  (void)threads;
+#endif
+}
+
 /* Restatement of setup_particles_scatter (src/main.rs:182-216) with a seeded Philox stream
  * in place of the unseeded rand::rng() (src/main.rs:188). */
 void orc_init_scatter(const rps_config* cfg, const rps_ext_config* ext, uint64_t seed,
@@ -522,6 +531,7 @@ void orc_sph_bin(const rps_config* cfg, const float* x, const float* y, uint32_t
                  uint32_t* offsets, uint32_t n) {
   const float x_max = cfg->screen_bounds[1], y_max = cfg->screen_bounds[3];
   const float r = cfg->smoothing_radius;
+#pragma omp parallel for schedule(static)
   for (uint32_t i = 0; i < n; ++i) {
     int32_t cx = orc_f32_to_i32((x[i] + x_max) / r);
     int32_t cy = orc_f32_to_i32((y[i] + y_max) / r);
@@ -549,6 +559,7 @@ uint32_t orc_sph_sort(uint32_t* lookup, uint32_t n) {
     for (uint32_t step = 0; step <= stage; ++step) {
       const uint32_t gw = 1u << (stage - step);
       const uint32_t gh = 2u * gw - 1u;
+#pragma omp parallel for schedule(static)
       for (uint32_t i = 0; i < P / 2u; ++i) {
         const uint32_t h = i & (gw - 1u);
         const uint32_t left = h + (gh + 1u) * (i / gw);
@@ -571,6 +582,7 @@ uint32_t orc_sph_sort(uint32_t* lookup, uint32_t n) {
 
 /* calculate_spatial_lookup_offsets (wgsl:507-525). */
 void orc_sph_offsets(const uint32_t* lookup, uint32_t* offsets, uint32_t n) {
+#pragma omp parallel for schedule(static) /* one writer per key: its run's first entry */
   for (uint32_t i = 0; i < n; ++i) {
     uint32_t key = lookup[2 * i];
     uint32_t prev = i > 0 ? lookup[2 * (i - 1)] : 0xFFFFFFFFu;
@@ -592,6 +604,7 @@ void orc_sph_pre(const rps_config* cfg, float* vx, float* vy, const float* x, co
                  uint32_t n) {
   const float dt = cfg->fixed_delta_time;
   const float gx_dt = 0.0f * dt, gy_dt = (-cfg->gravity) * dt;
+#pragma omp parallel for schedule(static)
   for (uint32_t i = 0; i < n; ++i) {
     vx[i] = vx[i] + gx_dt;
     vy[i] = vy[i] + gy_dt;
@@ -601,6 +614,7 @@ void orc_sph_pre(const rps_config* cfg, float* vx, float* vy, const float* x, co
   const float x_max = cfg->screen_bounds[1], y_max = cfg->screen_bounds[3];
   const float r = cfg->smoothing_radius, r2 = r * r;
   const uint32_t N = cfg->particle_count;
+#pragma omp parallel for schedule(dynamic, 1024)
   for (uint32_t i = 0; i < n; ++i) {
     const float px = pred[2 * i], py = pred[2 * i + 1];
     const int32_t cx = orc_f32_to_i32((px + x_max) / r);
@@ -648,6 +662,9 @@ void orc_sph_sim(const rps_config* cfg, float* x, float* y, float* vx, float* vy
   float* svy = (float*)malloc(sizeof(float) * n);
   memcpy(svx, vx, sizeof(float) * n);
   memcpy(svy, vy, sizeof(float) * n);
+  /* Iterations write only particle i and read neighbours from pred / dens / the velocity
+   * snapshot, so the OpenMP build (bench cpu_baseline) equals the serial checker bit for bit. */
+#pragma omp parallel for schedule(dynamic, 1024)
   for (uint32_t i = 0; i < n; ++i) {
     const float px = pred[2 * i], py = pred[2 * i + 1];
     const int32_t cx = orc_f32_to_i32((px + x_max) / r);

@@ -31,6 +31,8 @@ typedef struct orc_stats {
   uint64_t respawned;
 } orc_stats;
 
+/* Thread count of the OpenMP build (librps_oracle_omp.so); no-op in the serial checker. */
+void orc_set_threads(int threads);
 /* Random123 Philox4x32-10. */
 void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 /* Deterministic polynomial sin/cos of 2*pi*u, u in [0,1). */

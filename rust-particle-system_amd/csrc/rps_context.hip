@@ -1034,8 +1034,48 @@ int rps_time_steps(rps_ctx* ctx, uint32_t nsteps, double* total_ms) {
 
 void* rps_get_stream(rps_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 
-int rps_step_cost(const rps_ctx* ctx, double* amount, int* unit) {
-  if (!ctx || !amount || !unit) return fail(nullptr, RPS_ERR_INVALID_ARGUMENT, "null argument");
+static int sph_frame_cost(rps_ctx* ctx, rps_sph_cost* out) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!out) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "null output");
+  if (ctx->mode != RPS_MODE_SPH) return fail(ctx, RPS_ERR_UNSUPPORTED, "SPH mode only");
+  if (!ctx->have_config) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "rps_set_config first");
+  const SphBuffers b = sph_buffers(ctx);
+  // The counts read the last active frame's lookup, runs and predicted positions.
+  if (!ctx->active_steps) return fail(ctx, RPS_ERR_UNSUPPORTED, "run an active SPH frame first");
+  const uint32_t nb = sph_count_blocks(ctx->P);
+  unsigned long long* d = nullptr;
+  RPS_HIP(ctx, hipMalloc(&d, sizeof(unsigned long long) * 2 * nb));
+  std::vector<unsigned long long> h(2 * (size_t)nb);
+  hipError_t e = launch_sph_count(b, d, ctx->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(h.data(), d, h.size() * sizeof(h[0]), hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(ctx, RPS_ERR_DEVICE, std::string("SPH cost count: ") + hipGetErrorString(e));
+  uint64_t E = 0, W = 0;
+  for (uint32_t i = 0; i < nb; ++i) {
+    E += h[2 * (size_t)i];
+    W += h[2 * (size_t)i + 1];
+  }
+  const double P = (double)ctx->P, N = (double)ctx->n;
+  out->slots = ctx->P;
+  out->particles = ctx->n;
+  out->scanned_entries = E;
+  out->within_entries = W;
+  out->sort_launches = ctx->sort_launches;
+  out->sort_bytes = (double)ctx->sort_launches * P * 16.0 + N * 8.0;
+  out->predict_bytes = P * 60.0 + N * 8.0;
+  out->density_bytes = (double)E * 8.0 + P * 120.0;
+  out->sim_bytes = (double)E * 32.0 + P * 156.0;
+  out->frame_bytes = out->sort_bytes + out->predict_bytes + out->density_bytes + out->sim_bytes;
+  return RPS_OK;
+}
+
+int rps_sph_frame_cost(rps_ctx* ctx, rps_sph_cost* out) { return sph_frame_cost(ctx, out); }
+
+int rps_step_cost(const rps_ctx* cctx, double* amount, int* unit) {
+  if (!cctx || !amount || !unit) return fail(nullptr, RPS_ERR_INVALID_ARGUMENT, "null argument");
+  rps_ctx* ctx = const_cast<rps_ctx*>(cctx);  // SPH counts on the device (no state change)
   switch (ctx->mode) {
     case RPS_MODE_STREAM: {
       // r+w of x, y, vx, vy (+ the group's u16 [next] read, 2 B per 64 particles; the expiry
@@ -1049,8 +1089,14 @@ int rps_step_cost(const rps_ctx* ctx, double* amount, int* unit) {
       *amount = 20.0 * (double)ctx->n * (double)ctx->global_count;  // GPU Gems 3 ch.31 convention
       *unit = 1;
       return RPS_OK;
-    default:
-      return fail(const_cast<rps_ctx*>(ctx), RPS_ERR_UNSUPPORTED, "no closed-form cost for SPH mode");
+    default: {
+      rps_sph_cost c;
+      const int rc = sph_frame_cost(ctx, &c);
+      if (rc) return rc;
+      *amount = c.frame_bytes;
+      *unit = 0;
+      return RPS_OK;
+    }
   }
 }
 

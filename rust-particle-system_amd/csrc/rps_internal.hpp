@@ -130,6 +130,10 @@ hipError_t launch_sph_offsets(const SphBuffers& b, hipStream_t s);
 hipError_t launch_sph_pre(const SphBuffers& b, hipStream_t s, bool with_offsets);
 bool sph_fold_offsets();
 hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s);
+// Cost accounting (rps_sph_frame_cost): per workgroup of slots, the (scanned, within-radius)
+// neighbour entries of the current frame, as u64 pairs in out[2 * sph_count_blocks(p)].
+uint32_t sph_count_blocks(uint32_t p_slots);
+hipError_t launch_sph_count(const SphBuffers& b, unsigned long long* out, hipStream_t s);
 // Rebuild the per-particle predicted-position and density buffers from the slot records.
 hipError_t launch_sph_debug_views(const SphBuffers& b, hipStream_t s);
 

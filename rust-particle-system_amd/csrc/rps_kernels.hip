@@ -1119,6 +1119,55 @@ __global__ __launch_bounds__(kBlock) void sph_debug_views_kernel(SphSlots sl, f2
   dens[i] = sl.dens_s[t];
 }
 
+// Cost accounting for rps_sph_frame_cost (not on the frame path): per slot, the entries of
+// its particle's nine runs (what the reference's density and sim scans visit,
+// wgsl:207-254, :279-384) and how many of them lie within the radius.  One (scanned,
+// within) u64 pair per workgroup, summed on the host; integer sums, so order-free.
+__global__ __launch_bounds__(kBlock) void sph_count_kernel(const rps_config* __restrict__ cfg,
+                                                           const uint32_t* __restrict__ offsets,
+                                                           const uint32_t* __restrict__ ends,
+                                                           const f2* __restrict__ pp_s,
+                                                           uint32_t p_slots,
+                                                           unsigned long long* __restrict__ out) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  unsigned long long scanned = 0, within = 0;
+  if (t < p_slots) {
+    const f2 p = pp_s[t];
+    const float r = cfg->smoothing_radius, r2 = r * r;
+    const uint32_t N = cfg->particle_count;
+    const int32_t cx = f32_to_i32((p[0] + cfg->screen_bounds[1]) / r);
+    const int32_t cy = f32_to_i32((p[1] + cfg->screen_bounds[3]) / r);
+    for (int o = 0; o < 9; ++o) {
+      const uint32_t key = grid_key(cx, cy, o, N);
+      const uint32_t s0 = offsets[key];
+      if (s0 >= N) continue;
+      const uint32_t e0 = ends[key];
+      scanned += e0 - s0;
+      for (uint32_t j = s0; j < e0; ++j) {
+        const f2 q = pp_s[j];
+        const float dx = p[0] - q[0], dy = p[1] - q[1];
+        within += !((dx * dx + dy * dy) > r2);
+      }
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    scanned += __shfl_xor(scanned, off, 64);
+    within += __shfl_xor(within, off, 64);
+  }
+  __shared__ unsigned long long part[2][kBlock / 64];
+  const uint32_t wave = threadIdx.x / 64;
+  if ((threadIdx.x & 63u) == 0u) {
+    part[0][wave] = scanned;
+    part[1][wave] = within;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    unsigned long long v = 0;
+    for (uint32_t w = 0; w < kBlock / 64; ++w) v += part[threadIdx.x][w];
+    out[2ull * blockIdx.x + threadIdx.x] = v;
+  }
+}
+
 inline uint32_t blocks_for(uint64_t n, uint32_t per_block = kBlock) {
   return (uint32_t)((n + per_block - 1) / per_block);
 }
@@ -1469,6 +1518,14 @@ hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s) {
     default: RPS_SIM(8); break;
   }
 #undef RPS_SIM
+  return hipGetLastError();
+}
+
+uint32_t sph_count_blocks(uint32_t p_slots) { return blocks_for(p_slots); }
+
+hipError_t launch_sph_count(const SphBuffers& b, unsigned long long* out, hipStream_t s) {
+  hipLaunchKernelGGL(sph_count_kernel, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg, b.offsets, b.ends,
+                     b.sl.pp_s, b.p, out);
   return hipGetLastError();
 }
 

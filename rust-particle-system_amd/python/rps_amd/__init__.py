@@ -142,6 +142,18 @@ class Stats(ctypes.Structure):
 # --------------------------------------------------------------------------------------
 # Library loading (fail loudly; there is no fallback path)
 # --------------------------------------------------------------------------------------
+class SphCost(ctypes.Structure):
+    """rps_sph_cost: algorithmic bytes of one SPH frame (include/rps.h)."""
+    _fields_ = [("slots", ctypes.c_uint64), ("particles", ctypes.c_uint64),
+                ("scanned_entries", ctypes.c_uint64), ("within_entries", ctypes.c_uint64),
+                ("sort_launches", ctypes.c_uint64), ("sort_bytes", ctypes.c_double),
+                ("predict_bytes", ctypes.c_double), ("density_bytes", ctypes.c_double),
+                ("sim_bytes", ctypes.c_double), ("frame_bytes", ctypes.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 class RpsError(RuntimeError):
     def __init__(self, status: int, message: str):
         super().__init__(f"rps status {status}: {message}")
@@ -180,6 +192,7 @@ ABI_SYMBOLS = [
     ("rps_time_steps", _I, [_P, _U32, ctypes.POINTER(ctypes.c_double)]),
     ("rps_get_stream", _P, [_P]),
     ("rps_step_cost", _I, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I)]),
+    ("rps_sph_frame_cost", _I, [_P, ctypes.POINTER(SphCost)]),
     ("rps_comm_unique_id", _I, [_P]),
     ("rps_nbody_sources", _I, [_P, _I, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(_U64)]),
     ("rps_comm_init", _I, [_P, _I, _I, _P]),
@@ -517,6 +530,12 @@ class Context:
         amt, unit = ctypes.c_double(), ctypes.c_int()
         self._call("rps_step_cost", ctypes.byref(amt), ctypes.byref(unit))
         return amt.value, ("bytes" if unit.value == 0 else "flops")
+
+    def sph_frame_cost(self) -> dict:
+        """Algorithmic bytes of one SPH frame of the current state (rps_sph_frame_cost)."""
+        c = SphCost()
+        self._call("rps_sph_frame_cost", ctypes.byref(c))
+        return c.as_dict()
 
     def nbody_sources(self, pack: bool = True):
         """(device pointer, count) of the global float2 source array (rps_nbody_sources)."""

@@ -181,3 +181,54 @@ def test_sph_bench_workload_full_size(gpu, orc):
     soa = dict(x=parts["position"][:, 0].copy(), y=parts["position"][:, 1].copy(),
                vx=parts["velocity"][:, 0].copy(), vy=parts["velocity"][:, 1].copy())
     _frames_vs_oracle(rps, orc, n, soa, cfg, 2)
+
+
+@pytest.mark.parametrize("n", [4096, 3000])
+def test_sph_frame_cost_counts(gpu, orc, n):
+    """rps_sph_frame_cost's device counts (the roofline's E) equal the entries of every lookup
+    slot's nine runs, walked here on the oracle's lookup, offsets and predicted positions the
+    way the reference's scans walk them (wgsl:231-252): keys in the reference cell order, a
+    run ends at a key change or at N.  The byte model follows include/rps.h."""
+    import ref_numpy as RN
+
+    rps = gpu
+    cfg = rps.default_particle_config(n, gravity=100.0)
+    soa = _blob(n, 40 + n)
+    st = orc.SphState(n)
+    ref = copy_soa(soa)
+    with rps.Context(n, rps.MODE_SPH) as ctx:
+        ctx.set_config(cfg, rps.make_ext(shader_delay=0))
+        ctx.upload_soa(soa)
+        with pytest.raises(rps.RpsError):
+            ctx.sph_frame_cost()  # no active frame yet
+        ctx.step(1)
+        cost = ctx.sph_frame_cost()
+        amt, unit = ctx.step_cost()
+    st.grid(cfg, ref)
+    st.pre(cfg, ref)
+    P = st.P
+    lk = st.lookup.reshape(P, 2)
+    px, py = st.pred[0::2], st.pred[1::2]
+    r = F(cfg.smoothing_radius)
+    r2 = r * r
+    xm, ym = F(cfg.screen_bounds[1]), F(cfg.screen_bounds[3])
+    scanned = within = 0
+    for t in range(P):
+        i = int(lk[t, 1])
+        cx = RN.f32_to_i32((px[i] + xm) / r)
+        cy = RN.f32_to_i32((py[i] + ym) / r)
+        for ox, oy in RN.GRID_OFFSETS:
+            key = RN.hash_cell(cx + ox, cy + oy) % n
+            j = int(st.offsets[key])
+            while j < n and lk[j, 0] == key:
+                q = int(lk[j, 1])
+                dx, dy = px[i] - px[q], py[i] - py[q]
+                scanned += 1
+                within += int(not (dx * dx + dy * dy > r2))
+                j += 1
+    assert (cost["scanned_entries"], cost["within_entries"]) == (scanned, within)
+    assert cost["slots"] == P and cost["particles"] == n and cost["sort_launches"] >= 1
+    assert cost["density_bytes"] == 8.0 * scanned + 120.0 * P
+    assert cost["sim_bytes"] == 32.0 * scanned + 156.0 * P
+    assert unit == "bytes" and amt == cost["frame_bytes"]
+    assert cost["frame_bytes"] == cost["sort_bytes"] + cost["predict_bytes"] + cost["density_bytes"] + cost["sim_bytes"]

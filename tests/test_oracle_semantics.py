@@ -95,6 +95,25 @@ def test_omp_build_equals_serial(rps, orc):
     assert_soa_bitwise(a, b, keys=("x", "y", "vx", "vy", "exp"))
 
 
+@pytest.mark.parametrize("n", [20000, 1 << 15])
+def test_omp_sph_equals_serial(rps, orc, n):
+    """The OpenMP build of the five SPH passes (bench.py's SPH cpu_baseline) equals the serial
+    checker bit for bit: lookup, offsets, densities, predictions and state over 3 frames
+    (n = 20 000: non-pow2 pads)."""
+    cfg = rps.default_particle_config(n, gravity=100.0)
+    g = np.random.default_rng(n)
+    soa = dict(x=np.clip(g.normal(0, 200, n), -955, 955).astype(F), y=np.clip(g.normal(0, 120, n), -535, 535).astype(F),
+               vx=g.normal(0, 30, n).astype(F), vy=g.normal(0, 30, n).astype(F))
+    a, b = copy_soa(soa), copy_soa(soa)
+    sa, sb = orc.SphState(n), orc.SphState(n, omp=True, threads=4)
+    ext = rps.make_ext(shader_delay=0)
+    orc.run_steps(2, cfg, ext, a, 3, sph=sa)
+    orc.run_steps(2, cfg, ext, b, 3, sph=sb)
+    for name in ("lookup", "offsets", "dens", "pred"):
+        assert_bitwise(getattr(sb, name), getattr(sa, name), name)
+    assert_soa_bitwise(b, a)
+
+
 def test_run_steps_gating(rps, orc):
     # frame_count < SHADER_DELAY (=5) gates passes 4-5 (wgsl:426, :442): 4 inert steps.
     cfg = config_c1(rps, 256, gravity=9.8)
