@@ -1,0 +1,67 @@
+"""Same-box A/B of librps builds on SPH frames (run on the GPU box).
+
+    python tools/ab_sph.py [--n N] [--frames F] [--rounds R] LIB_A[@ENV=VAL...] LIB_B ...
+
+Each variant runs in its own subprocess (one librps per process), in rounds A, B, A, B, ...
+One run: N particles of the reference scatter over a viewport scaled to the default density
+(bench.py's `sph` workload), every frame active, 10 warm frames, F timed (HIP events)."""
+import json
+import os
+import statistics
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def one(lib, n, frames):
+    sys.path.insert(0, os.path.join(ROOT, "rust-particle-system_amd", "python"))
+    import rps_amd as rps
+
+    rps.LIB_PATH = os.path.abspath(lib)
+    scale = max(1.0, (n / 50000) ** 0.5)
+    cfg = rps.default_particle_config(n, screen_bounds=rps.screen_bounds_for(1920.0 * scale, 1080.0 * scale))
+    parts = rps.setup_particles_scatter(cfg, n, seed=0x5EED)
+    with rps.Context(n, rps.MODE_SPH) as ctx:
+        ctx.set_config(cfg, rps.make_ext(shader_delay=0))
+        ctx.upload(parts)
+        ctx.step(10)
+        ctx.sync()
+        ms = ctx.time_steps(frames) / frames
+    print(json.dumps({"lib": lib, "n": n, "ms_per_frame": ms}), flush=True)
+
+
+def main():
+    a = sys.argv[1:]
+    if a and a[0] == "--one":
+        one(a[1], int(a[2]), int(a[3]))
+        return
+    n, frames, rounds = 1 << 22, 50, 3
+    while a and a[0].startswith("--"):
+        if a[0] == "--n":
+            n = int(a[1])
+        elif a[0] == "--frames":
+            frames = int(a[1])
+        elif a[0] == "--rounds":
+            rounds = int(a[1])
+        a = a[2:]
+    res = {v: [] for v in a}
+    for _ in range(rounds):
+        for v in a:
+            lib, *envs = v.split("@")
+            env = dict(os.environ)
+            for e in envs:
+                k, val = e.split("=", 1)
+                env[k] = val
+            p = subprocess.run([sys.executable, __file__, "--one", lib, str(n), str(frames)], env=env,
+                               capture_output=True, text=True, timeout=600)
+            if p.returncode:
+                print(p.stderr[-2000:], flush=True)
+                sys.exit(p.returncode)
+            res[v].append(json.loads(p.stdout.strip().splitlines()[-1])["ms_per_frame"])
+    for v, ms in res.items():
+        print(f"n={n} {v}: median {statistics.median(ms):.4f} ms/frame  (runs {', '.join(f'{m:.4f}' for m in ms)})")
+
+
+if __name__ == "__main__":
+    main()
