@@ -45,7 +45,7 @@ struct rps_ctx {
   f4* st = nullptr;
   f4* st2 = nullptr;       // sim-pass output, swapped with st after the pass
   SphSlots sl{};           // SPH slot records (rps_internal.hpp)
-  uint2* bounds = nullptr;  // SPH: {offset, end} per key
+  uint32_t* ends = nullptr;
   uint2* lookup = nullptr;
   uint32_t* offsets = nullptr;
   f2* dens = nullptr;
@@ -269,7 +269,7 @@ SphBuffers sph_buffers(rps_ctx* ctx) {
   b.st = ctx->st;
   b.st2 = ctx->st2;
   b.sl = ctx->sl;
-  b.bounds = ctx->bounds;
+  b.ends = ctx->ends;
   b.lookup = ctx->lookup;
   b.offsets = ctx->offsets;
   b.dens = ctx->dens;
@@ -554,7 +554,7 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     slots.push_back({(void**)&ctx->sl.dens_s, align_up(P * sizeof(f2), 256)});
     slots.push_back({(void**)&ctx->sl.idx_s, align_up(P * sizeof(uint32_t), 256)});
     slots.push_back({(void**)&ctx->sl.cur_s, align_up(P * sizeof(f2), 256)});
-    slots.push_back({(void**)&ctx->bounds, align_up(n * sizeof(uint2), 256)});
+    slots.push_back({(void**)&ctx->ends, align_up(n * sizeof(uint32_t), 256)});
     slots.push_back({(void**)&ctx->sl.nbr_mask, align_up(2 * P * sizeof(uint64_t), 256)});
     slots.push_back({(void**)&ctx->lookup, align_up((size_t)ctx->P * sizeof(uint2), 256)});
     slots.push_back({(void**)&ctx->offsets, align_up(n * sizeof(uint32_t), 256)});
@@ -850,8 +850,6 @@ int rps_read_debug(rps_ctx* ctx, int which, void* dst, uint64_t bytes) {
   }
   if (which == RPS_DEBUG_DENSITIES || which == RPS_DEBUG_PREDICTED)
     RPS_HIP(ctx, launch_sph_debug_views(sph_buffers(ctx), ctx->stream));
-  if (which == RPS_DEBUG_LOOKUP_OFFSETS)
-    RPS_HIP(ctx, launch_sph_offsets_view(sph_buffers(ctx), ctx->stream));
   RPS_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
   RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return RPS_OK;

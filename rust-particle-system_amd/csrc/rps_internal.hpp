@@ -108,9 +108,8 @@ struct SphBuffers {
   const f4* st;      // N packed {x, y, vx, vy}: the state at the start of the frame
   f4* st2;           // N: sim-pass output (swapped with st after the pass)
   uint2* lookup;     // P entries
-  uint2* bounds;     // N: {first slot of each key's run (wgsl:55's offsets), one past its
-                     //     last slot in [0, N)}; one 8-B load per scanned run
-  uint32_t* offsets; // N: the reference's offsets buffer, a debug view of bounds[].x
+  uint32_t* offsets; // N: first slot of each key's run (wgsl:55)
+  uint32_t* ends;    // N: one past the last slot of each key's run in [0, N)
   f2* dens;          // N  debug views (wgsl:58, :61), rebuilt on readback
   f2* pred;          // N
   SphSlots sl;
@@ -137,7 +136,5 @@ uint32_t sph_count_blocks(uint32_t p_slots);
 hipError_t launch_sph_count(const SphBuffers& b, unsigned long long* out, hipStream_t s);
 // Rebuild the per-particle predicted-position and density buffers from the slot records.
 hipError_t launch_sph_debug_views(const SphBuffers& b, hipStream_t s);
-// offsets[key] = bounds[key].x, for rps_read_debug(RPS_DEBUG_LOOKUP_OFFSETS).
-hipError_t launch_sph_offsets_view(const SphBuffers& b, hipStream_t s);
 
 }  // namespace rps

@@ -637,12 +637,12 @@ struct PaddedTile {
 };
 
 // bin_particles_in_grid (wgsl:455-468) folded into the first sort launch: entries [0, n)
-// get (key, i) from the current positions and bounds[i].x (offsets[i]) <- 0xFFFFFFFF; entries [n, P) keep
+// get (key, i) from the current positions and offsets[i] <- 0xFFFFFFFF; entries [n, P) keep
 // what the previous frame's sort left there (the reference never rewrites them).
 struct SortBin {
   const rps_config* cfg;
   const f4* st;  // packed {x, y, vx, vy} per particle
-  uint2* bounds;
+  uint32_t* offsets;
   uint32_t n;
 };
 
@@ -651,7 +651,7 @@ __device__ __forceinline__ uint2 bin_entry(const SortBin& b, uint32_t i) {
   const f2 pos = reinterpret_cast<const f2*>(b.st)[2u * i];
   const int32_t cx = f32_to_i32((pos[0] + b.cfg->screen_bounds[1]) / r);
   const int32_t cy = f32_to_i32((pos[1] + b.cfg->screen_bounds[3]) / r);
-  b.bounds[i].x = 0xFFFFFFFFu;  // offsets[i] (the run end is read only for present keys)
+  b.offsets[i] = 0xFFFFFFFFu;
   return make_uint2(cell_key(cx, cy, b.cfg->particle_count), i);
 }
 
@@ -774,23 +774,16 @@ __global__ __launch_bounds__(1024) void sph_sort_local_kernel(
 // [offsets[key], ends[key]) is exactly the set of slots it visits, in the same order.
 // (ends[] needs no reset: it is read only for keys whose offsets entry this frame set.)
 __global__ __launch_bounds__(kBlock) void sph_offsets_kernel(const uint2* __restrict__ lookup,
-                                                             uint2* __restrict__ bounds,
+                                                             uint32_t* __restrict__ offsets,
+                                                             uint32_t* __restrict__ ends,
                                                              uint32_t n) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   const uint32_t key = lookup[i].x;
   const uint32_t prev = i > 0u ? lookup[i - 1u].x : 0xFFFFFFFFu;
   const uint32_t next = i + 1u < n ? lookup[i + 1u].x : 0xFFFFFFFFu;
-  if (key != prev) bounds[key].x = i;
-  if (key != next || i + 1u == n) bounds[key].y = i + 1u;
-}
-
-// The reference's spatial_lookup_offsets buffer (wgsl:55) for rps_read_debug.
-__global__ __launch_bounds__(kBlock) void sph_offsets_view_kernel(const uint2* __restrict__ bounds,
-                                                                  uint32_t* __restrict__ offsets,
-                                                                  uint32_t n) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i < n) offsets[i] = bounds[i].x;
+  if (key != prev) offsets[key] = i;
+  if (key != next || i + 1u == n) ends[key] = i + 1u;
 }
 
 __constant__ int32_t kGridOff[9][2] = {{-1, -1}, {-1, 0}, {-1, 1}, {0, -1}, {0, 0},
@@ -808,7 +801,8 @@ __global__ __launch_bounds__(kBlock) void sph_predict_kernel(const rps_config* _
                                                              const uint2* __restrict__ lookup,
                                                              const f4* __restrict__ st,
                                                              SphSlots sl, uint32_t p_slots,
-                                                             uint2* __restrict__ bounds,
+                                                             uint32_t* __restrict__ offsets,
+                                                             uint32_t* __restrict__ ends,
                                                              uint32_t n_offsets) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= p_slots) return;
@@ -816,8 +810,8 @@ __global__ __launch_bounds__(kBlock) void sph_predict_kernel(const rps_config* _
   if (t < n_offsets) {  // the offsets pass folded in (active frames): sph_offsets_kernel's body
     const uint32_t prev = t > 0u ? lookup[t - 1u].x : 0xFFFFFFFFu;
     const uint32_t next = t + 1u < n_offsets ? lookup[t + 1u].x : 0xFFFFFFFFu;
-    if (e.x != prev) bounds[e.x].x = t;
-    if (e.x != next || t + 1u == n_offsets) bounds[e.x].y = t + 1u;
+    if (e.x != prev) offsets[e.x] = t;
+    if (e.x != next || t + 1u == n_offsets) ends[e.x] = t + 1u;
   }
   const uint32_t i = e.y;
   const f4 s = st[i];
@@ -844,7 +838,8 @@ __device__ __forceinline__ uint32_t grid_key(int32_t cx, int32_t cy, int o, uint
                   (int32_t)((uint32_t)cy + (uint32_t)kGridOff[o][1]), N);
 }
 
-__device__ __forceinline__ uint32_t nine_runs(const uint2* __restrict__ bounds, float px, float py,
+__device__ __forceinline__ uint32_t nine_runs(const uint32_t* __restrict__ offsets,
+                                              const uint32_t* __restrict__ ends, float px, float py,
                                               float xoff, float yoff, float r, uint32_t N,
                                               RunTable& runs) {
   const int32_t cx = f32_to_i32((px + xoff) / r);  // particle_position_to_cell_coord, wgsl:121-130
@@ -854,9 +849,8 @@ __device__ __forceinline__ uint32_t nine_runs(const uint2* __restrict__ bounds, 
   for (int o = 0; o < 9; ++o) key[o] = grid_key(cx, cy, o, N);
 #pragma unroll
   for (int o = 0; o < 9; ++o) {
-    const uint2 be = bounds[key[o]];  // {offset, end}: one 8-B load per run
-    s[o] = be.x;
-    e[o] = be.y;
+    s[o] = offsets[key[o]];
+    e[o] = ends[key[o]];
   }
   uint32_t c = 0, m = 0;
 #pragma unroll
@@ -907,7 +901,8 @@ struct RunCursor {
 // predicted positions in flight per lane across run boundaries.
 template <int kScanBatch>
 __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* __restrict__ cfg,
-                                                             const uint2* __restrict__ bounds,
+                                                             const uint32_t* __restrict__ offsets,
+                                                             const uint32_t* __restrict__ ends,
                                                              SphSlots sl, uint32_t p_slots) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= p_slots) return;
@@ -916,7 +911,7 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
   const uint32_t N = cfg->particle_count;
   const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
   __shared__ RunTable runs;
-  const uint32_t total = nine_runs(bounds, p[0], p[1], cfg->screen_bounds[1],
+  const uint32_t total = nine_runs(offsets, ends, p[0], p[1], cfg->screen_bounds[1],
                                    cfg->screen_bounds[3], r, N, runs);
   RunCursor rc(runs);
   float d = 0.0f, nd = 0.0f;
@@ -1027,7 +1022,8 @@ __device__ __forceinline__ void scan_runs(const SphSlots& sl, const RunTable& ru
 // walls (:69-99).  The new packed state of particle i goes to st2[i].
 template <int kScanBatch, bool kPads>
 __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __restrict__ cfg,
-                                                         const uint2* __restrict__ bounds,
+                                                         const uint32_t* __restrict__ offsets,
+                                                         const uint32_t* __restrict__ ends,
                                                          SphSlots sl, f4* __restrict__ st2,
                                                          uint32_t p_slots) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
@@ -1047,7 +1043,7 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
   const float P_rho2 = own[2];             // loop-invariant halves of pressure_term and
   const float Pn_rho2 = Pn / (rho * rho);  // near_pressure_term (wgsl:323-327)
   __shared__ RunTable runs;
-  const uint32_t total = nine_runs(bounds, p[0], p[1], cfg->screen_bounds[1],
+  const uint32_t total = nine_runs(offsets, ends, p[0], p[1], cfg->screen_bounds[1],
                                    cfg->screen_bounds[3], r, N, runs);
   const bool masked = total <= 128u;
   const uint64_t m0 = masked ? sl.nbr_mask[t] : 0u, m1 = masked ? sl.nbr_mask[p_slots + t] : 0u;
@@ -1128,7 +1124,8 @@ __global__ __launch_bounds__(kBlock) void sph_debug_views_kernel(SphSlots sl, f2
 // wgsl:207-254, :279-384) and how many of them lie within the radius.  One (scanned,
 // within) u64 pair per workgroup, summed on the host; integer sums, so order-free.
 __global__ __launch_bounds__(kBlock) void sph_count_kernel(const rps_config* __restrict__ cfg,
-                                                           const uint2* __restrict__ bounds,
+                                                           const uint32_t* __restrict__ offsets,
+                                                           const uint32_t* __restrict__ ends,
                                                            const f2* __restrict__ pp_s,
                                                            uint32_t p_slots,
                                                            unsigned long long* __restrict__ out) {
@@ -1142,10 +1139,9 @@ __global__ __launch_bounds__(kBlock) void sph_count_kernel(const rps_config* __r
     const int32_t cy = f32_to_i32((p[1] + cfg->screen_bounds[3]) / r);
     for (int o = 0; o < 9; ++o) {
       const uint32_t key = grid_key(cx, cy, o, N);
-      const uint2 be = bounds[key];
-      const uint32_t s0 = be.x;
+      const uint32_t s0 = offsets[key];
       if (s0 >= N) continue;
-      const uint32_t e0 = be.y;
+      const uint32_t e0 = ends[key];
       scanned += e0 - s0;
       for (uint32_t j = s0; j < e0; ++j) {
         const f2 q = pp_s[j];
@@ -1398,7 +1394,7 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
     const int k = v && *v ? std::atoi(v) : 0;  // 0: by tile size (below)
     return k < 0 ? 0 : (k > 4 ? 4 : k);
   }();
-  const SortBin bin{b.cfg, b.st, b.bounds, b.n};
+  const SortBin bin{b.cfg, b.st, b.offsets, b.n};
   const SortBin nobin{nullptr, nullptr, nullptr, 0u};
   if (stages == 0) {  // P == 1: nothing to sort, only bin
     hipLaunchKernelGGL((sph_sort_local_kernel<true, 1>), dim3(1), dim3(64), 0, s, b.lookup, 1u, 1u, 0u,
@@ -1468,7 +1464,7 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
 
 hipError_t launch_sph_offsets(const SphBuffers& b, hipStream_t s) {
   hipLaunchKernelGGL(sph_offsets_kernel, dim3(blocks_for(b.n)), dim3(kBlock), 0, s, b.lookup,
-                     b.bounds, b.n);
+                     b.offsets, b.ends, b.n);
   return hipGetLastError();
 }
 
@@ -1493,12 +1489,12 @@ bool sph_fold_offsets() {
 
 hipError_t launch_sph_pre(const SphBuffers& b, hipStream_t s, bool with_offsets) {
   hipLaunchKernelGGL(sph_predict_kernel, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg, b.lookup,
-                     b.st, b.sl, b.p, b.bounds, with_offsets ? b.n : 0u);
+                     b.st, b.sl, b.p, b.offsets, b.ends, with_offsets ? b.n : 0u);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
 #define RPS_DENSITY(B)                                                                           \
   hipLaunchKernelGGL(sph_density_kernel<B>, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg, \
-                     b.bounds, b.sl, b.p)
+                     b.offsets, b.ends, b.sl, b.p)
   switch (sph_batch(true, b.p, b.batch_d)) {
     case 4: RPS_DENSITY(4); break;
     case 16: RPS_DENSITY(16); break;
@@ -1512,10 +1508,10 @@ hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s) {
 #define RPS_SIM(B)                                                                              \
   if (b.p == b.n)                                                                              \
     hipLaunchKernelGGL((sph_sim_kernel<B, false>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s,  \
-                       b.cfg, b.bounds, b.sl, b.st2, b.p);                            \
+                       b.cfg, b.offsets, b.ends, b.sl, b.st2, b.p);                            \
   else                                                                                         \
     hipLaunchKernelGGL((sph_sim_kernel<B, true>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s,   \
-                       b.cfg, b.bounds, b.sl, b.st2, b.p)
+                       b.cfg, b.offsets, b.ends, b.sl, b.st2, b.p)
   switch (sph_batch(false, b.p, b.batch_s)) {
     case 4: RPS_SIM(4); break;
     case 16: RPS_SIM(16); break;
@@ -1528,14 +1524,8 @@ hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s) {
 uint32_t sph_count_blocks(uint32_t p_slots) { return blocks_for(p_slots); }
 
 hipError_t launch_sph_count(const SphBuffers& b, unsigned long long* out, hipStream_t s) {
-  hipLaunchKernelGGL(sph_count_kernel, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg, b.bounds,
+  hipLaunchKernelGGL(sph_count_kernel, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg, b.offsets, b.ends,
                      b.sl.pp_s, b.p, out);
-  return hipGetLastError();
-}
-
-hipError_t launch_sph_offsets_view(const SphBuffers& b, hipStream_t s) {
-  hipLaunchKernelGGL(sph_offsets_view_kernel, dim3(blocks_for(b.n)), dim3(kBlock), 0, s, b.bounds, b.offsets,
-                     b.n);
   return hipGetLastError();
 }
 
