@@ -4,7 +4,8 @@
 
 Each variant runs in its own subprocess (one librps per process), in rounds A, B, A, B, ...
 One run: N particles of the reference scatter over a viewport scaled to the default density
-(bench.py's `sph` workload), every frame active, 10 warm frames, F timed (HIP events)."""
+(bench.py's `sph` workload), every frame active, 10 warm frames, F timed (HIP events).
+AB_MORTON=1 in a variant's environment uploads the particles in Morton order of their cells."""
 import json
 import os
 import statistics
@@ -22,6 +23,20 @@ def one(lib, n, frames):
     scale = max(1.0, (n / 50000) ** 0.5)
     cfg = rps.default_particle_config(n, screen_bounds=rps.screen_bounds_for(1920.0 * scale, 1080.0 * scale))
     parts = rps.setup_particles_scatter(cfg, n, seed=0x5EED)
+    if os.environ.get("AB_MORTON") == "1":  # upload in Morton order of the particles' cells
+        import numpy as np
+
+        r = float(cfg.smoothing_radius)
+        cx = ((parts["position"][:, 0] - cfg.screen_bounds[0]) / r).astype(np.uint64) & 0xFFFF
+        cy = ((parts["position"][:, 1] - cfg.screen_bounds[2]) / r).astype(np.uint64) & 0xFFFF
+
+        def spread(v):
+            v = (v | (v << 8)) & 0x00FF00FF
+            v = (v | (v << 4)) & 0x0F0F0F0F
+            v = (v | (v << 2)) & 0x33333333
+            return (v | (v << 1)) & 0x55555555
+
+        parts = parts[np.argsort(spread(cx) | (spread(cy) << np.uint64(1)), kind="stable")]
     with rps.Context(n, rps.MODE_SPH) as ctx:
         ctx.set_config(cfg, rps.make_ext(shader_delay=0))
         ctx.upload(parts)
