@@ -661,13 +661,13 @@ __device__ __forceinline__ uint2 bin_entry(const SortBin& b, uint32_t i) {
 template <int KMAX>
 __device__ __forceinline__ uint32_t sort_chunk(const PaddedTile& s, uint32_t off, uint32_t len,
                                                uint32_t stage, uint32_t step, uint32_t w0,
-                                               uint32_t wn) {
+                                               uint32_t wn, uint32_t cap = 32u) {
   const uint32_t G = 1u << (stage - step);
-  const uint32_t left = stage - step + 1u;  // passes left in this stage
+  const uint32_t left = min(stage - step + 1u, cap);  // passes left in this stage (capped)
   // A flip pass with G = 1 pairs (2i, 2i+1) exactly like a non-flip one.
   const bool flip = step == 0u && G > 1u;
   const uint32_t kf = KMAX > 1 ? (uint32_t)KMAX - 1u : 1u;  // flip chunks: 2^(K+1) entries
-  const uint32_t K = flip ? (G >= (2u << (kf - 1u)) ? kf : 1u)
+  const uint32_t K = flip ? ((G >= (2u << (kf - 1u)) && kf <= left) ? kf : 1u)
                           : (left < (uint32_t)KMAX ? left : (uint32_t)KMAX);
   const uint32_t g = G >> (K - 1u);
   const uint32_t groups = sort_groups(len, G, g, flip);
@@ -764,6 +764,46 @@ __global__ __launch_bounds__(1024) void sph_sort_local_kernel(
     }
   } else {
     for (uint32_t q = threadIdx.x; q < tile; q += blockDim.x) lookup[base0 + q] = s[q];
+  }
+}
+
+// All T global passes of one stage in one launch (T > 4 would take two or more register-fused
+// launches).  The passes have strides G = 2^s down to g = 2^lg (the LDS tile of the local
+// launches); as in sort_group, residue class r (positions r + j*g of a 2G block, j < 2^T)
+// together with its mirror class g-1-r is closed under them.  A workgroup takes 16
+// consecutive residues r0..r0+15 (r0 < g/2) and their mirrors: for each j one 128-B segment
+// of each class, 2^(T+5) entries in LDS.  In the tile's order tau = 32j + 16c + k (c = 1: the
+// mirror segment, ascending), which is the order of the original positions, the stage's flip
+// pass pairs tau with tile-1-tau and its stride g*2^m passes pair tau with tau + 32*2^m: the
+// passes of tile stage T+4 from step 0 down to group width 32.  Same network, same
+// compare-swaps, so the same result as T pass-per-dispatch launches.
+template <int KMAX, uint32_t CAP>
+__global__ __launch_bounds__(1024) void sph_sort_stage_kernel(uint2* __restrict__ lookup, uint32_t s,
+                                                              uint32_t lg, uint32_t T) {
+  __shared__ uint2 lds[CAP + CAP / 32];
+  const PaddedTile sm{lds};
+  const uint32_t tile = 32u << T;
+  const uint32_t g = 1u << lg;
+  const uint32_t rgs = lg - 5u;  // log2(residue groups of 16 in [0, g/2))
+  const uint32_t base = (blockIdx.x >> rgs) << (s + 1u);
+  const uint32_t r0 = (blockIdx.x & ((1u << rgs) - 1u)) << 4;
+  const auto pos = [&](uint32_t tau) {
+    const uint32_t j = tau >> 5, c = (tau >> 4) & 1u, k = tau & 15u;
+    return base + j * g + (c ? (g - 16u - r0 + k) : (r0 + k));
+  };
+  for (uint32_t q = 2u * threadIdx.x; q < tile; q += 2u * blockDim.x) {  // 16-B aligned pairs
+    const uint4 v = *reinterpret_cast<const uint4*>(lookup + pos(q));
+    sm[q] = make_uint2(v.x, v.y);
+    sm[q + 1u] = make_uint2(v.z, v.w);
+  }
+  __syncthreads();
+  for (uint32_t step = 0; step < T;) {
+    step += sort_chunk<KMAX>(sm, 0u, tile, T + 4u, step, threadIdx.x, blockDim.x, T - step);
+    __syncthreads();
+  }
+  for (uint32_t q = 2u * threadIdx.x; q < tile; q += 2u * blockDim.x) {
+    const uint2 a = sm[q], c = sm[q + 1u];
+    *reinterpret_cast<uint4*>(lookup + pos(q)) = make_uint4(a.x, a.y, c.x, c.y);
   }
 }
 
@@ -1417,6 +1457,13 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
     const int k = v && *v ? std::atoi(v) : 4;
     return (uint32_t)(k < 1 ? 1 : (k > 5 ? 5 : k));
   }();
+  // Stages with at least this many global passes run them in one gathered-tile launch
+  // (sph_sort_stage_kernel); RPS_SORT_GATHER_MIN=0 turns it off.
+  static const uint32_t gather_min = [] {
+    const char* v = std::getenv("RPS_SORT_GATHER_MIN");
+    const int k = v && *v ? std::atoi(v) : 5;
+    return k <= 0 ? 100u : (uint32_t)k;
+  }();
   const uint32_t want = tile_env ? tile_env : std::min(kSortTile, std::max(2048u, P / 256u));
   const uint32_t tile = P < want ? P : want;
   // Passes per register chunk: 3 on 8192-entry tiles, 2 on smaller ones (measured at 65 536
@@ -1438,6 +1485,21 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
     uint32_t T = 0;
     while (T <= stage && 2u * (1u << (stage - T)) > tile) ++T;
     uint32_t step = 0;
+    if (T >= gather_min && T <= 9u && tile_log >= 6u) {  // all T global passes, one launch
+      const uint32_t tt = 32u << T;
+      const uint32_t blocks = (P >> (stage + 1u)) << (tile_log - 5u);
+      const uint32_t threads = std::max(64u, std::min(1024u, tt >> 3));
+      if (tt > kSortTile)
+        hipLaunchKernelGGL((sph_sort_stage_kernel<3, kSortTileMax>), dim3(blocks), dim3(threads), 0, s,
+                           b.lookup, stage, tile_log, T);
+      else
+        hipLaunchKernelGGL((sph_sort_stage_kernel<3, kSortTile>), dim3(blocks), dim3(threads), 0, s,
+                           b.lookup, stage, tile_log, T);
+      e = hipGetLastError();
+      ++*launches;
+      if (e != hipSuccess) return e;
+      step = T;
+    }
     while (step < T) {
       const uint32_t k = T - step < fuse ? T - step : fuse;
       const uint32_t G = 1u << (stage - step);
