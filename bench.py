@@ -223,7 +223,7 @@ def allpairs(rps, args, d):
                       global_count=ng)
     try:
         ctx.set_config(cfg, ext)
-        if d.world > 1:
+        if d.dist:  # under a launcher, even with one rank: the library's own RCCL all-gather
             ctx.comm_init(d.rank, d.world, d.broadcast_bytes(rps.comm_unique_id() if d.rank == 0 else b""))
         ctx.init_scatter(args.seed)
         ctx.step(1)  # warm: RCCL channels, LDS kernels
@@ -249,7 +249,7 @@ def allpairs(rps, args, d):
             "interactions_per_s": inter / el, "force_kernel_ms": kms,
             "roofline": {"bound": "valu", "achieved": flop / (kms * 1e-3) / 1e12, "peak": 157.3,
                          "unit": "TFLOP/s", "frac": flop / (kms * 1e-3) / 1e12 / 157.3},
-            "collective": f"ncclAllGather {8 * ng} B per step" if d.world > 1 else "none (1 rank)"}
+            "collective": f"ncclAllGather {8 * ng} B per step" if d.dist else "none (no launcher)"}
 
 
 def sph_side(rps, args, d):
@@ -359,7 +359,7 @@ def main():
     ctx = rps.Context(n, rps.MODE_STREAM, device=d.local if d.dist else 0,
                       id_offset=d.rank * n, global_count=d.world * n)
     ctx.set_config(cfg, ext)
-    if d.world > 1:  # the stats steps all-reduce over the ranks inside librps (RCCL)
+    if d.dist:  # under a launcher the stats steps all-reduce over the ranks inside librps (RCCL)
         ctx.comm_init(d.rank, d.world, d.broadcast_bytes(rps.comm_unique_id() if d.rank == 0 else b""))
     ctx.init_scatter(args.seed)
     ctx.step(args.warmup)
@@ -379,7 +379,7 @@ def main():
     kern_ms = d.max(kern_ms)
     moved_per_launch, _ = ctx.step_cost()  # bytes the kernel moves: 32.03 B per particle
     algo_per_launch = ALGO_BYTES_PER_PARTICLE * n
-    if d.world > 1:
+    if d.dist:
         stats, stats_ok = stats_check(d, ctx.stats(), ctx.shard_stats())
     else:
         stats, stats_ok = global_stats(d, ctx.stats()), True

@@ -382,8 +382,9 @@ int step_nbody(rps_ctx* ctx) {
   // External exchange: the caller packed (rps_nbody_pack) and filled the other shards.
   if (!external)
     RPS_HIP(ctx, launch_nbody_pack(ctx->x, ctx->y, ctx->pos_all + ctx->id_offset, ctx->n, ctx->stream));
-  if (ctx->nranks > 1 && !external) {
-    // In-place all-gather of every rank's float2 positions over xGMI.
+  if (ctx->comm && !external) {
+    // In-place all-gather of every rank's float2 positions over xGMI; with one
+    // rank RCCL leaves the array as it is.
     ncclResult_t r = ncclAllGather(ctx->pos_all + ctx->id_offset, ctx->pos_all, ctx->n * 2,
                                    ncclFloat, ctx->comm, ctx->stream);
     if (r != ncclSuccess)
