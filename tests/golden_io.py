@@ -7,6 +7,9 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 STREAM = ("stream_c1_subset.npz", "stream_c1_attractor.npz", "stream_c2_verlet.npz", "stream_c3_features.npz")
 SPH = ("sph_n1000.npz", "sph_n2048.npz")
 NBODY = ("nbody_n1024.npz",)
+# Outputs of the reference's own compute_shader.wgsl (tests/golden/make_wgsl_golden.py):
+WGSL_SPH = ("wgsl_sph_n64.npz", "wgsl_sph_n100.npz", "wgsl_sph_n512_default.npz")
+WGSL_STREAM = ("wgsl_stream_c1_n128.npz",)
 
 
 def load(name):
@@ -29,6 +32,11 @@ def active_steps(g, ext):
         if f >= ext.shader_delay:
             out.append((f, len(out)))
     return out
+
+
+def wgsl_config(rps, g):
+    """A WGSL fixture's ParticleConfig (its ext is the reference's: no extensions, SHADER_DELAY 5)."""
+    return rps.ParticleConfig.from_buffer_copy(g["cfg"].tobytes()), rps.make_ext()
 
 
 def inputs(g):

@@ -4,7 +4,7 @@ Bitwise for STREAM and SPH; the DESIGN.md §3.4 tolerance for the all-pairs acce
 import numpy as np
 import pytest
 
-from golden_io import NBODY, SPH, STREAM, inputs, load, structs
+from golden_io import NBODY, SPH, STREAM, WGSL_SPH, WGSL_STREAM, inputs, load, structs, wgsl_config
 from helpers import assert_bitwise, assert_soa_bitwise
 from test_gpu_nbody import _check_accel
 
@@ -76,3 +76,50 @@ def test_nbody_golden_gpu(gpu, orc, name):
     assert_soa_bitwise(got, ref)
     for k in ("x", "y", "vx", "vy"):
         np.testing.assert_allclose(got[k], g["out_" + k], rtol=1e-4, atol=1e-3)
+
+
+def _check_gpu_frame(rps, ctx, g, f, n, sph):
+    got = ctx.download_soa()
+    for k in ("x", "y", "vx", "vy"):
+        assert_bitwise(got[k], g[f"f{f}_{k}"], f"{k} f{f}")
+    assert_bitwise(ctx.download()["color"].reshape(-1), g[f"f{f}_color"].reshape(-1), f"colour f{f}")
+    if sph:
+        assert_bitwise(ctx.read_debug(rps.DEBUG_SPATIAL_LOOKUP), g[f"f{f}_lookup"], f"lookup f{f}")
+        assert_bitwise(ctx.read_debug(rps.DEBUG_LOOKUP_OFFSETS), g[f"f{f}_offsets"], f"offsets f{f}")
+        if f >= 5:
+            assert_bitwise(ctx.read_debug(rps.DEBUG_PREDICTED), g[f"f{f}_pred"], f"pred f{f}")
+            assert_bitwise(ctx.read_debug(rps.DEBUG_DENSITIES), g[f"f{f}_dens"], f"dens f{f}")
+
+
+@pytest.mark.parametrize("name", WGSL_SPH)
+def test_wgsl_sph_golden_gpu(gpu, name):
+    """librps against outputs of the reference's own compute_shader.wgsl (tests/wgsl_interp.py,
+    make_wgsl_golden.py): every buffer of every frame, bitwise."""
+    rps = gpu
+    g = load(name)
+    cfg, ext = wgsl_config(rps, g)
+    soa = inputs(g)
+    n = len(soa["x"])
+    with rps.Context(n, rps.MODE_SPH) as ctx:
+        ctx.set_config(cfg, ext)
+        ctx.upload_soa(soa)
+        for f in range(1, int(g["frames"][0]) + 1):
+            ctx.step(1)
+            _check_gpu_frame(rps, ctx, g, f, n, True)
+
+
+@pytest.mark.parametrize("name", WGSL_STREAM)
+def test_wgsl_stream_golden_gpu(gpu, name):
+    """The STREAM mode with no extensions against the reference shader's particles (pressure,
+    near-pressure and viscosity multipliers zero), frame by frame."""
+    rps = gpu
+    g = load(name)
+    cfg, ext = wgsl_config(rps, g)
+    soa = inputs(g)
+    n = len(soa["x"])
+    with rps.Context(n, rps.MODE_STREAM) as ctx:
+        ctx.set_config(cfg, ext)
+        ctx.upload_soa(soa)
+        for f in range(1, int(g["frames"][0]) + 1):
+            ctx.step(1)
+            _check_gpu_frame(rps, ctx, g, f, n, False)

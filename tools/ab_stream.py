@@ -5,7 +5,7 @@
 Each library runs in its own subprocess (one librps per process), in rounds A, B, A, B, ...
 so drift of the box (clocks, temperature) hits every variant alike.  One run: the bench's
 C3 workload (1e8 particles, headline_ext with stats, seeded scatter), 100 warm-up steps,
-500 timed.  Prints one JSON line per run and the per-library medians."""
+500 timed.  AB_ATTRACTORS / AB_LIFE in a variant's environment trim the workload.  Prints one JSON line per run and the per-library medians."""
 import json
 import os
 import statistics
@@ -24,6 +24,12 @@ def one(lib, fuse, n=100_000_000, warm=100, steps=500):
     ext = rps.headline_ext(stats=True)
     ext.shader_delay = 0
     ext.fuse_steps = fuse
+    # Workload knobs for attributing the step's time (a variant's @ENV=VAL):
+    # AB_ATTRACTORS=k keeps the first k attractors, AB_LIFE=0 turns the lifetime off.
+    if "AB_ATTRACTORS" in os.environ:
+        ext.num_attractors = min(ext.num_attractors, int(os.environ["AB_ATTRACTORS"]))
+    if os.environ.get("AB_LIFE") == "0":
+        ext.flags &= ~rps.EXT_LIFETIME
     with rps.Context(n) as ctx:
         ctx.set_config(cfg, ext)
         ctx.init_scatter(0x5EED)
