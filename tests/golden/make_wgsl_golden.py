@@ -72,6 +72,15 @@ def main():
     case("wgsl_sph_n512_default.npz", cfg,
          dict(x=parts["position"][:, 0].copy(), y=parts["position"][:, 1].copy(),
               vx=parts["velocity"][:, 0].copy(), vy=parts["velocity"][:, 1].copy()), 6)
+    # SPH with particles far beyond the walls (cells off the grid, hashed like any other) and
+    # a non-default radius and viewport.
+    n = 200
+    cfg = rps.default_particle_config(n, gravity=100.0, smoothing_radius=14.0,
+                                      screen_bounds=rps.screen_bounds_for(2400.0, 1400.0))
+    soa = blob(n, 8)
+    soa["x"][:6] = F(2000.0)
+    soa["y"][6:12] = F(-3000.0)
+    case("wgsl_sph_n200_outside.npz", cfg, soa, 7)
     # The streaming reference subset (C1): pressure, near-pressure and viscosity multipliers
     # zero, so each active frame is gravity -> Euler -> walls -> colour; particles on and
     # beyond the walls.
