@@ -64,6 +64,8 @@ def main():
     case("wgsl_sph_n64.npz", rps.default_particle_config(64, gravity=100.0), blob(64, 5), 7)
     # SPH, non-pow2 N: the next_pow2 lookup's zero pad entries sort into [0, N).
     case("wgsl_sph_n100.npz", rps.default_particle_config(100, gravity=100.0), blob(100, 6), 7)
+    # ... run until a particle pushed out of [0, N) has density 0 and its NaN spreads.
+    case("wgsl_sph_n100_nan.npz", rps.default_particle_config(100, gravity=100.0), blob(100, 6), 11)
     # SPH at the reference defaults (gravity 0, default density), the reference scatter.
     n = 512
     scale = (n / 50000) ** 0.5
