@@ -538,6 +538,8 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     // Tiled SoA: ceil(n / kTile) tiles of 4 f32 + 2 u16 segments (rps_device.hpp).
     const size_t tiles = (n + kTile - 1) / kTile;
     slots.push_back({(void**)&ctx->state, tiles * kTileBytes});
+    slots.push_back({(void**)&ctx->exp, align_up(tiles * kTile * sizeof(uint16_t), 256)});
+    slots.push_back({(void**)&ctx->next, align_up((tiles * kTile >> kGroupLog) * sizeof(uint16_t), 256)});
   } else if (ctx->mode == RPS_MODE_NBODY) {
     slots.push_back({(void**)&ctx->x, nf});
     slots.push_back({(void**)&ctx->y, nf});
@@ -598,8 +600,7 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     ctx->y = ctx->state + kTile;
     ctx->vx = ctx->state + 2 * kTile;
     ctx->vy = ctx->state + 3 * kTile;
-    ctx->exp = reinterpret_cast<uint16_t*>(ctx->state + 4 * kTile);
-    ctx->next = ctx->exp + kTile;  // zero-filled with the arena: expiries 0, clock 0, next 0
+    // exp / next: arrays of their own, zero-filled with the arena (expiries 0, clock 0, next 0)
     ctx->exp_layout = tiled_exp_layout();
   }
   // wgpu buffers are zero-initialised; the SPH lookup pad entries rely on it.

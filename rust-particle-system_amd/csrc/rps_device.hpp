@@ -19,19 +19,21 @@ constexpr int kMaxAttractors = 8;
 
 // Particle-state layout in HBM.  STREAM mode keeps the state as *tiled SoA*
 // (AoSoA): tiles of kTile particles, each tile holding four contiguous f32 segments
-// [x | y | vx | vy], one u16 segment [expiry] and one u16 segment [next] with an entry per
-// group of 64 particles: the group's earliest expiry, so a step reads the expiries only in
-// the group-steps where one of them is due (kTile * 18.5 B = 148 KiB per tile).  Lanes read
-// 16 contiguous bytes of each f32 field (16 lanes share a [next] entry); a workgroup's streams fall in one
-// tile instead of arrays gigabytes apart (tools/hbm_probe.hip: 6.35-6.39 TB/s tiled vs
-// 5.3 TB/s plain SoA on the in-place update).  SPH and N-body keep plain SoA.
+// [x | y | vx | vy] (128 KiB).  Lanes read 16 contiguous bytes of each field; a workgroup's
+// streams fall in one tile instead of arrays gigabytes apart (tools/hbm_probe.hip: 6.35-6.6
+// TB/s tiled vs 5.3 TB/s plain SoA on the in-place update).  The u16 lifetime expiries and
+// the [next] index (one u16 per group of 64 particles: the group's earliest expiry, so a
+// step reads the expiries only in the group-steps where one of them is due) are plain arrays
+// of their own: inside the tiles they stretched the f32 tile stride from 128 to 148 KiB, and
+// the C3 step ran 3.2 % slower (0.5112 -> 0.4949 ms, same box).  SPH and N-body keep plain SoA.
 constexpr uint32_t kTileLog = 13;
 constexpr uint64_t kTile = 1ull << kTileLog;
-constexpr uint64_t kTileBytes = kTile * 37 / 2;  // 4 x f32 + 1 x u16 per particle + u16 per quad
+constexpr uint64_t kTileBytes = kTile * 16;  // 4 x f32 per particle (the u16 expiry and [next]
+                                             // are arrays of their own)
 
 // Element offset of particle i inside one field: (((i & ~mask) * mult) >> shift) + (i & mask).
-// plain: mask = ~0 (offset i).  Tiled f32 fields: the tile stride is 4.625 * kTile floats
-// (mult 37, shift 3); the tiled u16 expiry: 9.25 * kTile u16 (mult 37, shift 2).
+// plain: mask = ~0 (offset i).  Tiled f32 fields: the tile stride is 4 * kTile floats
+// (mult 32, shift 3).  The expiry and [next] arrays are plain.
 struct Layout {
   uint64_t mask;
   uint64_t mult;
@@ -41,26 +43,21 @@ __host__ __device__ __forceinline__ uint64_t lidx(Layout L, uint64_t i) {
   return (((i & ~L.mask) * L.mult) >> L.shift) + (i & L.mask);
 }
 __host__ __device__ __forceinline__ Layout plain_layout() { return Layout{~0ull, 1, 0}; }
-__host__ __device__ __forceinline__ Layout tiled_layout() { return Layout{kTile - 1, 37, 3}; }
-__host__ __device__ __forceinline__ Layout tiled_exp_layout() { return Layout{kTile - 1, 37, 2}; }
+__host__ __device__ __forceinline__ Layout tiled_layout() { return Layout{kTile - 1, 32, 3}; }
+__host__ __device__ __forceinline__ Layout tiled_exp_layout() { return plain_layout(); }
 // Tiled offsets with compile-time constants (the stream kernel's address math).
 __device__ __forceinline__ uint64_t tidx(uint64_t i) {
-  return (((i & ~(kTile - 1)) * 37) >> 3) + (i & (kTile - 1));
+  return ((i & ~(kTile - 1)) << 2) + (i & (kTile - 1));
 }
-__device__ __forceinline__ uint64_t eidx(uint64_t i) {
-  return (((i & ~(kTile - 1)) * 37) >> 2) + (i & (kTile - 1));
-}
+__device__ __forceinline__ uint64_t eidx(uint64_t i) { return i; }
 // [next] holds one entry per group of kGroup particles (16 quads: the 16 lanes of a DPP row),
 // so a step reads 2 B per 64 particles of it.  A group's expiries are 128 B, one cache line,
 // and the lines of due groups are the ones that move either way: per-quad entries (0.5 B per
-// particle) bought nothing over this but their own traffic.  The segment keeps kTile / 4
-// entries per tile; the first kTile / kGroup are used.
+// particle) bought nothing over this but their own traffic.
 constexpr uint32_t kGroupLog = 6;
 constexpr uint64_t kGroup = 1ull << kGroupLog;
-// [next] entry of the group holding particle i (from the [next] segment of tile 0).
-__host__ __device__ __forceinline__ uint64_t nidx(uint64_t i) {
-  return (((i & ~(kTile - 1)) * 37) >> 2) + ((i & (kTile - 1)) >> kGroupLog);
-}
+// [next] entry of the group holding particle i.
+__host__ __device__ __forceinline__ uint64_t nidx(uint64_t i) { return i >> kGroupLog; }
 // Earliest expiry of a quad as seen at lifetime clock c: the expiry e with the smallest
 // (u16)(e - c), i.e. the next step in which one of the four respawns.
 __host__ __device__ __forceinline__ uint16_t quad_next(uint16_t e0, uint16_t e1, uint16_t e2,
@@ -73,7 +70,7 @@ __host__ __device__ __forceinline__ uint16_t quad_next(uint16_t e0, uint16_t e1,
 }
 
 // Base pointers of the fields; for the tiled layout f32 field f starts at tile-0 offset
-// f * kTile floats and the expiry at byte 4 * kTile * 4.
+// f * kTile floats; the expiry array is plain.
 struct Fields {
   float* x;
   float* y;
