@@ -414,7 +414,10 @@ def main():
                      "avg_kernel_ms": kern_ms, "launches": launches,
                      "algorithmic_bytes_per_launch": algo_per_launch,
                      "moved_bytes_per_launch": moved_per_launch, "moved_gbps": moved_gbps,
-                     "moved_frac": moved_gbps / HBM_PEAK_GBPS},
+                     "moved_frac": moved_gbps / HBM_PEAK_GBPS,
+                     "note": "achieved/frac use SURVEY 8(d)'s 40 algorithmic bytes per particle-step; the "
+                             "kernel moves 32.03 of them (u16 expiry behind a per-group index), so frac can "
+                             "exceed 1; moved_frac is the HBM utilisation"},
         "stats": stats,
     }
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
