@@ -343,8 +343,8 @@ __device__ __forceinline__ void stream_body(const StreamArgs& a, att_ptr att0, s
 }
 
 template <bool VERLET, bool LIFETIME, bool STATS, int NTM>
-// No occupancy cap: 74 VGPRs (6 waves/SIMD) measured 0.9 % faster than the same code held to
-// 64 VGPRs (8 waves) by amdgpu_waves_per_eu(7) (tools/ab_stream.py, same box).
+// Occupancy is capped at 6 waves/SIMD by the launcher's LDS reservation (launch_stream_t), not
+// by register limits: 8 waves are slower than 6 on this stream whatever the VGPR count.
 __global__ __launch_bounds__(kBlock) void stream_step_kernel(StreamArgs a) {
   stream_body<VERLET, LIFETIME, STATS, NTM>(a, kernarg_f4<StreamArgs>(offsetof(StreamArgs, att)), 0, 1);
 }
@@ -1230,13 +1230,16 @@ uint32_t stream_blocks_for(uint64_t n) {
 
 template <bool V, bool L, bool S, int NTM>
 static hipError_t launch_stream_t(const StreamArgs& a, uint32_t grid, hipStream_t s) {
-  // RPS_STREAM_LDS: LDS bytes reserved per workgroup and never used, an occupancy cap for
-  // experiments (default 0 = none).  28 000 B admits 5 workgroups per CU (5 waves/SIMD; 74
-  // VGPRs alone allow 6): 0.5084 -> 0.5059 ms per 1e8 step on one box, 0.5114 -> 0.5118 on
-  // another; 4 (32 KiB, 36 000 B) and 3 waves were 3 % and 11 % slower (tools/ab_stream.py).
+  // An LDS reservation that is never used caps the occupancy at 6 workgroups per CU (6
+  // waves/SIMD; 163 840 / 25 000 = 6.55).  The kernels at <= 64 VGPRs (no lifetime, no stats)
+  // otherwise run 8 waves/SIMD, and 8 is slower than 6 on the stream (same box, 1e8,
+  // tools/ab_stream.py, AB_LIFE=0): 8 waves 0.5051 ms, 7 0.5004, 6 0.4767, 5 0.4766, 4
+  // 0.4854.  The C3 kernel (71 VGPRs, 7 waves) is unchanged at 6 (0.4923 vs 0.4924) and
+  // slower at 5 (0.5050) and 4 (0.5358); the stats steps (83-91 VGPRs) run 5 either way.
+  // RPS_STREAM_LDS=<bytes> overrides it (0 = no cap).
   static const uint32_t lds = [] {
     const char* v = std::getenv("RPS_STREAM_LDS");
-    const long k = v && *v ? std::atol(v) : 0;
+    const long k = v && *v ? std::atol(v) : 25000;
     return (uint32_t)(k < 0 ? 0 : (k > 65536 ? 65536 : k));
   }();
   hipLaunchKernelGGL((stream_step_kernel<V, L, S, NTM>), dim3(grid), dim3(kBlock), lds, s, a);
