@@ -142,6 +142,19 @@ int env_int(const char* name, int dflt) {
   return v && *v ? std::atoi(v) : dflt;
 }
 
+// Default cache policy of the stream step (bit 0 nontemporal loads, bit 1 nontemporal
+// stores) from the 32 B/particle of state the step streams.  Nontemporal stores always;
+// loads temporal while the state is within about twice the 256-MB Infinity Cache (MALL),
+// which then still serves part of each step's reads.  Same box, C2 ext, us/step, both
+// nontemporal vs temporal loads (tools/ab_stream.py AB_C2=1 AB_N=n RPS_STREAM_NT=3/2):
+//   2^20 (32 MiB) 6.00 / 6.44     2^21 11.25 / 9.48     2^22 22.37 / 21.29
+//   2^23 42.89 / 39.38            2^24 (512 MiB) 82.48 / 75.03
+//   20 Mi (640 MiB) 102.8 / 107.0 24 Mi 122.3 / 131.3   2^25 162.1 / 176.0   1e8 479 / 522
+int stream_nt_default(uint64_t n) {
+  const uint64_t bytes = n * 32;
+  return (bytes > (48ull << 20) && bytes <= (576ull << 20)) ? 2 : 3;
+}
+
 int check_ctx(rps_ctx* ctx) {
   if (!ctx) return fail(nullptr, RPS_ERR_INVALID_ARGUMENT, "null context");
   hipError_t e = hipSetDevice(ctx->device);
@@ -504,7 +517,7 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
   ctx->global_count = global;
   ctx->ext = default_ext();
   ctx->stream_grid = (uint32_t)std::max(0, env_int("RPS_STREAM_GRID", 0));
-  ctx->nontemporal = env_int("RPS_STREAM_NT", 3) & 3;  // bit 0 loads, bit 1 stores
+  ctx->nontemporal = env_int("RPS_STREAM_NT", stream_nt_default(ctx->n)) & 3;
   ctx->xcd_order = env_int("RPS_STREAM_XCD", 0) != 0;  // measured slower
   // Tuning knobs read per context (A/B sweeps, and tests that force a variant at small N).
   {
