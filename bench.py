@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--allpairs-n", type=int, default=1 << 22,
                     help="global particles of the all-pairs N-body side measurement (0: skip)")
     ap.add_argument("--allpairs-steps", type=int, default=2)
+    ap.add_argument("--allpairs-cpu-n", type=int, default=65536,
+                    help="all-pairs CPU baseline size (SURVEY 8d: 65 536, every target x every source; 0: skip)")
     ap.add_argument("--sph-n", type=int, default=1 << 22,
                     help="particles of the SPH-frame side measurement per rank (0: skip)")
     ap.add_argument("--sph-frames", type=int, default=50)
@@ -249,7 +251,35 @@ def allpairs(rps, args, d):
             "interactions_per_s": inter / el, "force_kernel_ms": kms,
             "roofline": {"bound": "valu", "achieved": flop / (kms * 1e-3) / 1e12, "peak": 157.3,
                          "unit": "TFLOP/s", "frac": flop / (kms * 1e-3) / 1e12 / 157.3},
-            "collective": f"ncclAllGather {8 * ng} B per step" if d.dist else "none (no launcher)"}
+            "collective": f"ncclAllGather {8 * ng} B per step" if d.dist else "none (no launcher)",
+            **({"cpu_baseline": allpairs_cpu_baseline(rps, args, ext)}
+               if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline and args.allpairs_cpu_n > 0 else {})}
+
+
+def allpairs_cpu_baseline(rps, args, ext):
+    """SURVEY 8(d)'s all-pairs CPU baseline: the same softened-gravity force at N = 65 536
+    (every target against every source), f32, vectorised with OpenMP on the host cores
+    (oracle/rps_oracle.c orc_nbody_accel_f32_omp), repeated for about 3 s.  Interactions/s; the
+    rate at 2^22 or 2^24 is this one extrapolated (the work per interaction does not depend on N)."""
+    import numpy as np
+    import oracle as orc
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    n = args.allpairs_cpu_n
+    g = np.random.default_rng(args.seed)
+    sx = g.uniform(-960.0, 960.0, n).astype(np.float32)
+    sy = g.uniform(-540.0, 540.0, n).astype(np.float32)
+    orc.nbody_accel_f32_omp(ext, sx, sy, nt=min(n, 1024), threads=threads)  # warm
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        orc.nbody_accel_f32_omp(ext, sx, sy, threads=threads)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= 3.0 or reps >= 100:
+            break
+    return {"value": float(n) * n * reps / el, "unit": "interactions/s", "cores": threads, "kind": "port",
+            "sample": f"{n} x {n} interactions x {reps} (f32, oracle/rps_oracle.c orc_nbody_accel_f32_omp, "
+                      f"-O3 -fopenmp omp simd, {threads} threads), {el:.1f} s; extrapolated to {args.allpairs_n}"}
 
 
 def sph_side(rps, args, d):

@@ -54,6 +54,7 @@ def lib(omp: bool = False) -> ctypes.CDLL:
         "orc_stream_step_omp": (None, [_P, _P, _U64, _U64, _U32, _P, _P, _P, _P, _P, _U64, _I]),
         "orc_init_scatter": (None, [_P, _P, _U64, _U64, _U64, _U32, _P, _P, _P, _P, _P, _U64]),
         "orc_nbody_accel": (None, [_P, _P, _P, _U64, _U64, _U64, _P, _P]),
+        "orc_nbody_accel_f32_omp": (None, [_P, _P, _P, _U64, _U64, _U64, _P, _P, _I]),
         "orc_nbody_integrate": (None, [_P, _P, _P, _P, _P, _P, _P, _P, _U64]),
         "orc_sph_bin": (None, [_P, _P, _P, _P, _P, _U32]),
         "orc_sph_sort": (_U32, [_P, _U32]),
@@ -208,6 +209,17 @@ def nbody_accel(ext, sx, sy, t0=0, nt=None):
     ax = np.zeros(nt, np.float32)
     ay = np.zeros(nt, np.float32)
     lib().orc_nbody_accel(_ref(ext), _p(sx), _p(sy), len(sx), t0, nt, _p(ax), _p(ay))
+    return ax, ay
+
+
+def nbody_accel_f32_omp(ext, sx, sy, t0=0, nt=None, threads=0):
+    """f32 all-pairs force on every host core (bench cpu_baseline; its own summation order)."""
+    sx = np.ascontiguousarray(sx, np.float32)
+    sy = np.ascontiguousarray(sy, np.float32)
+    nt = len(sx) - t0 if nt is None else nt
+    ax = np.zeros(nt, np.float32)
+    ay = np.zeros(nt, np.float32)
+    lib(omp=True).orc_nbody_accel_f32_omp(_ref(ext), _p(sx), _p(sy), len(sx), t0, nt, _p(ax), _p(ay), threads)
     return ax, ay
 
 

@@ -497,6 +497,30 @@ void orc_nbody_accel(const rps_ext_config* ext, const float* sx, const float* sy
   }
 }
 
+void orc_nbody_accel_f32_omp(const rps_ext_config* ext, const float* sx, const float* sy,
+                             uint64_t ns, uint64_t t0, uint64_t nt, float* ax, float* ay,
+                             int threads) {
+  const float eps2 = ext->nbody_softening * ext->nbody_softening;
+  const float gm = ext->nbody_strength;
+  orc_set_threads(threads);
+#pragma omp parallel for schedule(dynamic, 64)
+  for (uint64_t ii = 0; ii < nt; ++ii) {
+    const float xi = sx[t0 + ii], yi = sy[t0 + ii];
+    float accx = 0.0f, accy = 0.0f;
+#pragma omp simd reduction(+ : accx, accy)
+    for (uint64_t j = 0; j < ns; ++j) {
+      const float dx = sx[j] - xi, dy = sy[j] - yi;
+      const float r2 = dx * dx + dy * dy + eps2;
+      const float inv = 1.0f / sqrtf(r2);
+      const float s = inv * inv * inv;
+      accx += dx * s;
+      accy += dy * s;
+    }
+    ax[ii] = accx * gm;
+    ay[ii] = accy * gm;
+  }
+}
+
 void orc_nbody_integrate(const rps_config* cfg, const rps_ext_config* ext, const float* ax,
                          const float* ay, float* x, float* y, float* vx, float* vy, uint64_t n) {
   step_consts k;
