@@ -192,3 +192,19 @@ def test_nbody_oracle_matches_direct_sum(rps, orc):
     sx, sy = orc.nbody_accel(ext, x, y, t0=100, nt=50)
     assert_bitwise(sx, ax[100:150])
     assert_bitwise(sy, ay[100:150])
+
+
+def test_nbody_f32_baseline_port_close_to_oracle(rps, orc):
+    """bench.py's all-pairs cpu_baseline computes the same force (f32, its own summation
+    order): within f32 rounding of the f64-accumulated oracle."""
+    ext = rps.make_ext(nbody_strength=1.0e5, nbody_softening=1.0, shader_delay=0)
+    g = np.random.default_rng(9)
+    x = g.uniform(-960, 960, 2000).astype(F)
+    y = g.uniform(-540, 540, 2000).astype(F)
+    ax, ay = orc.nbody_accel(ext, x, y)
+    bx, by = orc.nbody_accel_f32_omp(ext, x, y, threads=2)
+    err = np.hypot(bx - ax, by - ay) / np.hypot(ax, ay)
+    assert float(np.median(err)) < 1e-5 and float(err.max()) < 1e-3
+    tx, ty = orc.nbody_accel_f32_omp(ext, x, y, t0=500, nt=100, threads=2)
+    assert_bitwise(tx, bx[500:600])
+    assert_bitwise(ty, by[500:600])
