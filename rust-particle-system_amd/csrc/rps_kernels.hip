@@ -1552,13 +1552,21 @@ bool sph_fold_offsets() {
   return f;
 }
 
+// Experiment knob: LDS bytes reserved (never used) on a scan launch, an occupancy cap.
+static uint32_t sph_lds_extra(const char* name) {
+  const char* v = std::getenv(name);
+  const long k = v && *v ? std::atol(v) : 0;
+  return (uint32_t)(k < 0 ? 0 : (k > 65536 ? 65536 : k));
+}
+
 hipError_t launch_sph_pre(const SphBuffers& b, hipStream_t s, bool with_offsets) {
+  static const uint32_t lds_d = sph_lds_extra("RPS_SPH_DENSITY_LDS");
   hipLaunchKernelGGL(sph_predict_kernel, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg, b.lookup,
                      b.st, b.sl, b.p, b.offsets, b.ends, with_offsets ? b.n : 0u);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
 #define RPS_DENSITY(B)                                                                           \
-  hipLaunchKernelGGL(sph_density_kernel<B>, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg, \
+  hipLaunchKernelGGL(sph_density_kernel<B>, dim3(blocks_for(b.p)), dim3(kBlock), lds_d, s, b.cfg, \
                      b.offsets, b.ends, b.sl, b.p)
   switch (sph_batch(true, b.p, b.batch_d)) {
     case 4: RPS_DENSITY(4); break;
@@ -1570,12 +1578,13 @@ hipError_t launch_sph_pre(const SphBuffers& b, hipStream_t s, bool with_offsets)
 }
 
 hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s) {
+  static const uint32_t lds_s = sph_lds_extra("RPS_SPH_SIM_LDS");
 #define RPS_SIM(B)                                                                              \
   if (b.p == b.n)                                                                              \
-    hipLaunchKernelGGL((sph_sim_kernel<B, false>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s,  \
+    hipLaunchKernelGGL((sph_sim_kernel<B, false>), dim3(blocks_for(b.p)), dim3(kBlock), lds_s, s, \
                        b.cfg, b.offsets, b.ends, b.sl, b.st2, b.p);                            \
   else                                                                                         \
-    hipLaunchKernelGGL((sph_sim_kernel<B, true>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s,   \
+    hipLaunchKernelGGL((sph_sim_kernel<B, true>), dim3(blocks_for(b.p)), dim3(kBlock), lds_s, s, \
                        b.cfg, b.offsets, b.ends, b.sl, b.st2, b.p)
   switch (sph_batch(false, b.p, b.batch_s)) {
     case 4: RPS_SIM(4); break;
