@@ -29,6 +29,7 @@ import wgsl_harness as H  # noqa: E402
 from helpers import config_c1, random_soa  # noqa: E402
 
 F = np.float32
+ONLY = sys.argv[1:]  # regenerate just these fixtures (file names); default: all
 
 
 def raw(struct):
@@ -43,6 +44,8 @@ def blob(n, seed):
 
 
 def case(name, cfg, soa, frames):
+    if ONLY and name not in ONLY:
+        return
     out = H.run_reference(cfg, soa, frames)
     d = dict(cfg=raw(cfg), frames=np.array([frames]))
     for k in ("x", "y", "vx", "vy"):
@@ -83,6 +86,13 @@ def main():
     soa["x"][:6] = F(2000.0)
     soa["y"][6:12] = F(-3000.0)
     case("wgsl_sph_n200_outside.npz", cfg, soa, 7)
+    # Tiny N: P = 1 (no sort pass), 2, 4 (one pad) and 32 (15 pads); a lone particle is its
+    # own only neighbour.
+    for n, seed in ((1, 21), (2, 22), (3, 23), (17, 24)):
+        soa = blob(n, seed)
+        soa["x"] *= F(0.2)
+        soa["y"] *= F(0.2)
+        case(f"wgsl_sph_n{n}_tiny.npz", rps.default_particle_config(n, gravity=100.0), soa, 7)
     # The streaming reference subset (C1): pressure, near-pressure and viscosity multipliers
     # zero, so each active frame is gravity -> Euler -> walls -> colour; particles on and
     # beyond the walls.

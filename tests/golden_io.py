@@ -8,7 +8,8 @@ STREAM = ("stream_c1_subset.npz", "stream_c1_attractor.npz", "stream_c2_verlet.n
 SPH = ("sph_n1000.npz", "sph_n2048.npz")
 NBODY = ("nbody_n1024.npz",)
 # Outputs of the reference's own compute_shader.wgsl (tests/golden/make_wgsl_golden.py):
-WGSL_SPH = ("wgsl_sph_n64.npz", "wgsl_sph_n100.npz", "wgsl_sph_n512_default.npz", "wgsl_sph_n200_outside.npz",
+WGSL_SPH = ("wgsl_sph_n1_tiny.npz", "wgsl_sph_n2_tiny.npz", "wgsl_sph_n3_tiny.npz", "wgsl_sph_n17_tiny.npz",
+            "wgsl_sph_n64.npz", "wgsl_sph_n100.npz", "wgsl_sph_n512_default.npz", "wgsl_sph_n200_outside.npz",
             "wgsl_sph_n100_nan.npz")
 WGSL_STREAM = ("wgsl_stream_c1_n128.npz",)
 

@@ -20,7 +20,7 @@ def _blob(n, seed, spread=None):
                 vx=g.normal(0, 30, n).astype(F), vy=g.normal(0, 30, n).astype(F))
 
 
-@pytest.mark.parametrize("n", [64, 1000, 4096, 50000, 65536])
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 17, 64, 1000, 4096, 50000, 65536])
 def test_sph_steps_bitwise(gpu, orc, n):
     rps = gpu
     cfg = rps.default_particle_config(n, gravity=100.0)
