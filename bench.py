@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--sph-cpu-n", type=int, default=1 << 22,
                     help="particles of the SPH CPU-baseline sample (oracle, OpenMP)")
     ap.add_argument("--sph-cpu-frames", type=int, default=3)
+    ap.add_argument("--export-reps", type=int, default=20,
+                    help="render-interop export (rps_export_particles) repetitions timed on the headline state; 0: skip")
     ap.add_argument("--allpairs-timeout", type=float, default=240.0,
                     help="watchdog: print the headline line and exit non-zero if a side run hangs")
     ap.add_argument("--master-port", type=int, default=0,
@@ -358,6 +360,48 @@ def sph_cpu_baseline(rps, args):
                       f"-O3 -fopenmp, {threads} threads), {el:.1f} s; {el * 1e3 / args.sph_cpu_frames:.0f} ms/frame"}
 
 
+def export_side(ctx, n, reps):
+    """SURVEY 8(f)3, render interop: rps_export_particles writes the headline state as the
+    reference's 32-B Particle buffer (render_shader.wgsl:26-30; colour derived, set_color)
+    into device memory, on the context stream.  Timed with HIP events on that stream over
+    `reps` exports of all n particles; algorithmic bytes 48 per particle (16 read, 32 written)."""
+    import ctypes
+
+    hip = ctypes.CDLL("libamdhip64.so.7")  # the runtime librps already loaded
+    vp = ctypes.c_void_p
+    hip.hipMalloc.argtypes = [ctypes.POINTER(vp), ctypes.c_size_t]
+    hip.hipFree.argtypes = [vp]
+    hip.hipEventCreate.argtypes = [ctypes.POINTER(vp)]
+    hip.hipEventRecord.argtypes = [vp, vp]
+    hip.hipEventSynchronize.argtypes = [vp]
+    hip.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), vp, vp]
+    hip.hipEventDestroy.argtypes = [vp]
+    buf, e0, e1 = vp(), vp(), vp()
+    if hip.hipMalloc(ctypes.byref(buf), n * 32) != 0:
+        return {"error": "hipMalloc of the export buffer failed"}
+    try:
+        assert hip.hipEventCreate(ctypes.byref(e0)) == 0 and hip.hipEventCreate(ctypes.byref(e1)) == 0
+        stream = vp(ctx.stream_ptr())
+        ctx.export_particles(buf.value)  # warm
+        hip.hipEventRecord(e0, stream)
+        for _ in range(reps):
+            ctx.export_particles(buf.value)
+        hip.hipEventRecord(e1, stream)
+        assert hip.hipEventSynchronize(e1) == 0
+        ms = ctypes.c_float()
+        hip.hipEventElapsedTime(ctypes.byref(ms), e0, e1)
+        per = ms.value / reps
+        gbps = 48.0 * n / (per * 1e-3) / 1e9
+        return {"what": "rps_export_particles: SoA state -> 32-B AoS Particle (render_shader.wgsl:26-30) in device memory",
+                "particles": n, "reps": reps, "ms_per_export": per, "particles_per_s": n / (per * 1e-3),
+                "roofline": {"bound": "hbm", "achieved": gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                             "frac": gbps / HBM_PEAK_GBPS, "algorithmic_bytes": 48.0 * n}}
+    finally:
+        hip.hipEventDestroy(e0)
+        hip.hipEventDestroy(e1)
+        hip.hipFree(buf)
+
+
 def stats_check(d, st_all, st_shard):
     """With more than one rank the stream context holds an RCCL communicator, and librps
     all-reduces every stats step itself (rps_get_stats).  Its result must equal the same
@@ -409,6 +453,7 @@ def main():
     kern_ms = d.max(kern_ms)
     moved_per_launch, _ = ctx.step_cost()  # bytes the kernel moves: 32.03 B per particle
     algo_per_launch = ALGO_BYTES_PER_PARTICLE * n
+    export = export_side(ctx, n, args.export_reps) if args.export_reps > 0 and hasattr(ctx, "stream_ptr") else None
     if d.dist:
         stats, stats_ok = stats_check(d, ctx.stats(), ctx.shard_stats())
     else:
@@ -450,6 +495,8 @@ def main():
                              "exceed 1; moved_frac is the HBM utilisation"},
         "stats": stats,
     }
+    if export is not None:
+        line["export"] = export
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(rps, args, cfg, ext)
     sides = [("sph", sph_side, args.sph_n > 0), ("allpairs", allpairs, args.allpairs_n > 0)]

@@ -442,6 +442,10 @@ class Context:
         n = self.n - offset if n is None else n
         self._call("rps_export_particles", ctypes.c_void_p(device_ptr), offset, n)
 
+    def stream_ptr(self) -> int:
+        """The context's hipStream_t (rps_get_stream), for callers that order work on it."""
+        return int(lib().rps_get_stream(self._p) or 0)
+
     def upload_field(self, field_id: int, values: np.ndarray, offset: int = 0):
         v = np.ascontiguousarray(values, dtype=np.float32)
         self._call("rps_upload_field", field_id, _fptr(v), offset, len(v))
