@@ -13,7 +13,7 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_BUILD = os.path.join(_HERE, "_build")
+_BUILD = os.environ.get("RPS_ORACLE_BUILD") or os.path.join(_HERE, "_build")  # override: sanitizer builds
 _libs = {}
 
 _P, _U32, _U64, _I, _F = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, ctypes.c_float
