@@ -1472,20 +1472,35 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
     return k <= 0 ? 100u : (uint32_t)k;
   }();
   const uint32_t want = tile_env ? tile_env : std::min(kSortTile, std::max(2048u, P / 256u));
-  const uint32_t tile = P < want ? P : want;
+  uint32_t tile = P < want ? P : want;
   // Passes per register chunk: 3 on 8192-entry tiles, 2 on smaller ones (measured at 65 536
   // to 2^22 particles; 4 is slower everywhere: fewer waves per CU).
-  const int kmax = kmax_env ? kmax_env : (tile >= kSortTile ? 3 : 2);
+  int kmax = kmax_env ? kmax_env : (tile >= kSortTile ? 3 : 2);
   uint32_t tile_log = 0;
   while ((1u << tile_log) < tile) ++tile_log;
-  const uint32_t tiles = P / tile;
+  uint32_t tiles = P / tile;
   // Stages whose whole network fits one tile: one launch (with the bin pass).
   const uint32_t first_global_stage = tile_log;  // stage s has 2*2^s = 2^(s+1) span
-  const uint32_t lt = std::max(64u, std::min(1024u, tile >> kmax));
+  uint32_t lt = std::max(64u, std::min(1024u, tile >> kmax));
   hipError_t e = launch_sort_local(kmax, true, tiles, lt, s, b.lookup, tile, 0u, first_global_stage - 1u,
                                    0u, bin);
   ++*launches;
   if (e != hipSuccess) return e;
+  // Tile of the later stages' local launches (RPS_SORT_TILE2; default: the first launch's).
+  // A smaller one moves one more pass per stage into the global launches.
+  static const uint32_t tile2_env = [] {
+    const char* v = std::getenv("RPS_SORT_TILE2");
+    const uint32_t t = v && *v ? (uint32_t)std::atoi(v) : 0u;
+    return (t >= 64u && t <= kSortTileMax && (t & (t - 1u)) == 0u) ? t : 0u;
+  }();
+  if (tile2_env && tile2_env < tile) {
+    tile = tile2_env;
+    tile_log = 0;
+    while ((1u << tile_log) < tile) ++tile_log;
+    tiles = P / tile;
+    kmax = kmax_env ? kmax_env : (tile >= kSortTile ? 3 : 2);
+    lt = std::max(64u, std::min(1024u, tile >> kmax));
+  }
   for (uint32_t stage = first_global_stage; stage < stages; ++stage) {
     // Passes whose compare span 2*gw exceeds the tile are global: steps [0, T).  They run
     // in register-fused chunks of up to `fuse` passes (sph_sort_fused_kernel).
