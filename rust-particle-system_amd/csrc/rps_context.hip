@@ -43,7 +43,6 @@ struct rps_ctx {
   uint16_t* next = nullptr;        // STREAM: per-quad earliest expiry (rps_device.hpp)
   // SPH: packed {x, y, vx, vy} state (x..vy point into st, layout sph_layout())
   f4* st = nullptr;
-  f4* st2 = nullptr;       // sim-pass output, swapped with st after the pass
   SphSlots sl{};           // SPH slot records (rps_internal.hpp)
   uint32_t* ends = nullptr;
   uint2* lookup = nullptr;
@@ -280,7 +279,6 @@ SphBuffers sph_buffers(rps_ctx* ctx) {
   SphBuffers b;
   b.cfg = ctx->d_cfg;
   b.st = ctx->st;
-  b.st2 = ctx->st2;
   b.sl = ctx->sl;
   b.ends = ctx->ends;
   b.lookup = ctx->lookup;
@@ -450,8 +448,6 @@ int step_sph_sim(rps_ctx* ctx, bool with_offsets) {
   RPS_HIP(ctx, launch_sph_sim(b, ctx->stream));
   rc = prof_end(ctx);
   if (rc) return rc;
-  std::swap(ctx->st, ctx->st2);
-  set_sph_fields(ctx);
   return RPS_OK;
 }
 
@@ -563,7 +559,6 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     ctx->P = next_pow2_u32((uint32_t)n);  // spatial lookup sized next_pow2 (particle_buffers.rs:86)
     const size_t P = ctx->P;
     slots.push_back({(void**)&ctx->st, align_up(n * sizeof(f4), 256)});
-    slots.push_back({(void**)&ctx->st2, align_up(n * sizeof(f4), 256)});
     slots.push_back({(void**)&ctx->sl.pp_s, align_up(P * sizeof(f2), 256)});
     slots.push_back({(void**)&ctx->sl.rec_pv, align_up(P * sizeof(f4), 256)});
     slots.push_back({(void**)&ctx->sl.rec_pd, align_up(P * sizeof(f4), 256)});

@@ -105,8 +105,7 @@ struct SphSlots {
 };
 struct SphBuffers {
   const rps_config* cfg;  // device-resident ParticleConfig
-  const f4* st;      // N packed {x, y, vx, vy}: the state at the start of the frame
-  f4* st2;           // N: sim-pass output (swapped with st after the pass)
+  f4* st;            // N packed {x, y, vx, vy}: read by bin/predict, written in place by the sim
   uint2* lookup;     // P entries
   uint32_t* offsets; // N: first slot of each key's run (wgsl:55)
   uint32_t* ends;    // N: one past the last slot of each key's run in [0, N)

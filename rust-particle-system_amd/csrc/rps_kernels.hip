@@ -1063,12 +1063,16 @@ __device__ __forceinline__ void scan_runs(const SphSlots& sl, const RunTable& ru
 
 // simulation_step, compute_shader.wgsl:435-453: pressure (:256-334) and viscosity
 // (:336-384) against the start-of-pass velocity snapshot (rec_pv.zw), Euler (:392-395) and
-// walls (:69-99).  The new packed state of particle i goes to st2[i].
+// walls (:69-99).  The new packed state of particle i is written in place, st[i]: after the
+// predict pass nothing reads st in this frame (the scans read the slot records), so one state
+// buffer does; a second one (ping-pong) only added 64 MB at 2^22 to the frame's working set,
+// which is what decides whether the scattered 16-B writes merge in the Infinity Cache or go
+// to HBM as partial-line writes.
 template <int kScanBatch, bool kPads>
 __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __restrict__ cfg,
                                                          const uint32_t* __restrict__ offsets,
                                                          const uint32_t* __restrict__ ends,
-                                                         SphSlots sl, f4* __restrict__ st2,
+                                                         SphSlots sl, f4* __restrict__ st,
                                                          uint32_t p_slots) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= p_slots) return;
@@ -1148,7 +1152,7 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
   float oy = c[1] + qy * dt;
   wall(cfg->screen_bounds[0], cfg->screen_bounds[1], cfg->screen_bounds[2], cfg->screen_bounds[3],
        cfg->damping_factor, ox, oy, qx, qy);
-  st2[i] = f4{ox, oy, qx, qy};
+  st[i] = f4{ox, oy, qx, qy};
 }
 
 // predicted_positions / densities (wgsl:58, :61) rebuilt from the slot records for
@@ -1601,10 +1605,10 @@ hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s) {
 #define RPS_SIM(B)                                                                              \
   if (b.p == b.n)                                                                              \
     hipLaunchKernelGGL((sph_sim_kernel<B, false>), dim3(blocks_for(b.p)), dim3(kBlock), lds_s, s, \
-                       b.cfg, b.offsets, b.ends, b.sl, b.st2, b.p);                            \
+                       b.cfg, b.offsets, b.ends, b.sl, b.st, b.p);                            \
   else                                                                                         \
     hipLaunchKernelGGL((sph_sim_kernel<B, true>), dim3(blocks_for(b.p)), dim3(kBlock), lds_s, s, \
-                       b.cfg, b.offsets, b.ends, b.sl, b.st2, b.p)
+                       b.cfg, b.offsets, b.ends, b.sl, b.st, b.p)
   switch (sph_batch(false, b.p, b.batch_s)) {
     case 4: RPS_SIM(4); break;
     case 16: RPS_SIM(16); break;
