@@ -17,6 +17,20 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 
 constexpr int kMaxAttractors = 8;
 
+// Correctly rounded sqrt for x == 0, x >= 2^-96, +inf and NaN (payload aside): the
+// compiler's IEEE sequence without its input scaling for tiny x.  v_sqrt_f32 is within
+// 1 ulp; the two FMA residual tests pick the correctly rounded neighbour exactly as that
+// sequence does.  Callers take sqrtf for 0 < x < 2^-96 (tools/sqrt_check.hip compares this
+// with sqrtf over every non-negative float on the GPU).
+__device__ __forceinline__ float sqrt_rn_unscaled(float x) {
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float sdn = __int_as_float(__float_as_int(s) - 1);
+  const float sup = __int_as_float(__float_as_int(s) + 1);
+  float t = (__builtin_fmaf(-sdn, s, x) <= 0.0f) ? sdn : s;
+  t = (__builtin_fmaf(-sup, s, x) > 0.0f) ? sup : t;
+  return t;
+}
+
 // Particle-state layout in HBM.  STREAM mode keeps the state as *tiled SoA*
 // (AoSoA): tiles of kTile particles, each tile holding four contiguous f32 segments
 // [x | y | vx | vy] (128 KiB).  Lanes read 16 contiguous bytes of each field; a workgroup's
