@@ -1516,7 +1516,16 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
     uint32_t T = 0;
     while (T <= stage && 2u * (1u << (stage - T)) > tile) ++T;
     uint32_t step = 0;
-    if (T >= gather_min && T <= 9u && tile_log >= 6u) {  // all T global passes, one launch
+    // Five global passes: one register-fused launch (32 entries per thread) once P gives it
+    // 2^17 threads; the gathered-tile launch below otherwise (2^22 frame 1.2352 -> 1.2248 ms;
+    // at 2^20 and 65 536 the fused launch is slower: 0.3852 -> 0.3882, 0.1157 -> 0.1213).
+    if (T == 5u && P >= (1u << 22) && fuse >= 4u) {
+      e = launch_sort_fused<5>(b.lookup, P, 1u << stage, true, s);
+      ++*launches;
+      if (e != hipSuccess) return e;
+      step = T;
+    }
+    if (step < T && T >= gather_min && T <= 9u && tile_log >= 6u) {  // all T global passes, one launch
       const uint32_t tt = 32u << T;
       const uint32_t blocks = (P >> (stage + 1u)) << (tile_log - 5u);
       const uint32_t threads = std::max(64u, std::min(1024u, tt >> 3));
