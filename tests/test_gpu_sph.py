@@ -168,13 +168,14 @@ def test_sph_forced_scan_batches(gpu, orc, monkeypatch, n, batch):
     _frames_vs_oracle(rps, orc, n, _blob(n, n + 2), cfg, 3)
 
 
-def test_sph_bench_workload_full_size(gpu, orc):
-    """The bench's `sph` workload exactly: 2^22 particles of the reference scatter over a
+@pytest.mark.parametrize("n", [1 << 22, 1 << 21])
+def test_sph_bench_workload_full_size(gpu, orc, n):
+    """The bench's `sph` workload exactly (2^22): particles of the reference scatter over a
     viewport scaled to the default density, every frame active.  P > 2^21 selects the sim
-    scan's 8-entry batch and 8192-entry sort tiles with 3 passes per register chunk; two
-    frames, every pass bitwise."""
+    scan's 8-entry batch, 8192-entry sort tiles with 3 passes per register chunk and the
+    five-pass register-fused global stage; at P = 2^21 (the largest size on the 4-entry sim
+    batch) that stage is a gathered-tile launch.  Two frames, every pass bitwise."""
     rps = gpu
-    n = 1 << 22
     scale = (n / 50000) ** 0.5
     cfg = rps.default_particle_config(n, screen_bounds=rps.screen_bounds_for(1920.0 * scale, 1080.0 * scale))
     parts = rps.setup_particles_scatter(cfg, n, seed=0x5EED)
