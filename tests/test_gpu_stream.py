@@ -115,6 +115,40 @@ def test_headline_features_bitwise(gpu, orc):
         assert_bitwise(ctx.read_debug(rps.DEBUG_EXPIRY), ref["exp"], "expiry")
 
 
+_WRAP_N, _WRAP_STEPS = 4099, 70000
+
+
+@pytest.fixture(scope="module")
+def wrap_case(gpu, orc):
+    """Inputs and the oracle's state after _WRAP_STEPS C3 steps (shared by both launch modes)."""
+    rps = gpu
+    cfg = config_c1(rps, _WRAP_N)
+    ext = rps.headline_ext()
+    ext.shader_delay = 0
+    soa = random_soa(_WRAP_N, list(cfg.screen_bounds), seed=77, life=(-0.05, 0.2))
+    ref = copy_soa(soa)
+    for s in range(_WRAP_STEPS):
+        orc.stream_step(cfg, ext, ref, s)
+    return cfg, ext, soa, ref
+
+
+@pytest.mark.parametrize("fuse", [1, 16])
+def test_lifetime_clock_wraps(gpu, wrap_case, fuse):
+    """The lifetime clock is a u16: expiries and the per-group [next] index
+    compare modulo 2^16.  70 000 C3 steps carry it once around (clock 65 535 -> 0) with
+    respawns in flight; every field and the raw expiries stay bitwise with the oracle, one
+    step per launch and 16 fused per launch, at a ragged N (tail lanes included)."""
+    rps = gpu
+    cfg, ext, soa, ref = wrap_case
+    ext.fuse_steps = fuse
+    with _gpu_ctx(rps, _WRAP_N, cfg, ext, soa) as ctx:
+        ctx.step(_WRAP_STEPS)
+        got = ctx.download_soa(life=True)
+        exp = ctx.read_debug(rps.DEBUG_EXPIRY)
+    assert_soa_bitwise(got, ref, keys=KEYS5)
+    assert_bitwise(exp, ref["exp"], "expiry")
+
+
 @pytest.mark.parametrize("n", [1, 3, 5, 63, 1023, 4097, 65539])
 def test_ragged_sizes(gpu, orc, n):
     rps = gpu
