@@ -380,16 +380,19 @@ def export_side(ctx, n, reps):
     if hip.hipMalloc(ctypes.byref(buf), n * 32) != 0:
         return {"error": "hipMalloc of the export buffer failed"}
     try:
-        assert hip.hipEventCreate(ctypes.byref(e0)) == 0 and hip.hipEventCreate(ctypes.byref(e1)) == 0
+        if hip.hipEventCreate(ctypes.byref(e0)) != 0 or hip.hipEventCreate(ctypes.byref(e1)) != 0:
+            raise RuntimeError("hipEventCreate failed")
         stream = vp(ctx.stream_ptr())
         ctx.export_particles(buf.value)  # warm
-        hip.hipEventRecord(e0, stream)
+        if hip.hipEventRecord(e0, stream) != 0:
+            raise RuntimeError("hipEventRecord failed")
         for _ in range(reps):
             ctx.export_particles(buf.value)
-        hip.hipEventRecord(e1, stream)
-        assert hip.hipEventSynchronize(e1) == 0
+        if hip.hipEventRecord(e1, stream) != 0 or hip.hipEventSynchronize(e1) != 0:
+            raise RuntimeError("hipEventRecord/Synchronize failed")
         ms = ctypes.c_float()
-        hip.hipEventElapsedTime(ctypes.byref(ms), e0, e1)
+        if hip.hipEventElapsedTime(ctypes.byref(ms), e0, e1) != 0:
+            raise RuntimeError("hipEventElapsedTime failed")
         per = ms.value / reps
         gbps = 48.0 * n / (per * 1e-3) / 1e9
         return {"what": "rps_export_particles: SoA state -> 32-B AoS Particle (render_shader.wgsl:26-30) in device memory",
@@ -397,8 +400,10 @@ def export_side(ctx, n, reps):
                 "roofline": {"bound": "hbm", "achieved": gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                              "frac": gbps / HBM_PEAK_GBPS, "algorithmic_bytes": 48.0 * n}}
     finally:
-        hip.hipEventDestroy(e0)
-        hip.hipEventDestroy(e1)
+        ctx.sync()  # no export still writing into the buffer
+        for ev in (e0, e1):
+            if ev.value:
+                hip.hipEventDestroy(ev)
         hip.hipFree(buf)
 
 
