@@ -631,6 +631,8 @@ __global__ __launch_bounds__(kBlock) void sph_sort_fused_kernel(uint2* __restric
 
 constexpr uint32_t kSortTile = 8192;      // entries per workgroup tile (64 KiB of LDS)
 constexpr uint32_t kSortTileMax = 16384;  // largest tile (132 KiB of LDS, one workgroup per CU)
+constexpr uint32_t kSortLd = 8;           // 16-B tile loads a lane keeps in flight at once
+constexpr uint32_t kSortLdBin = 4;        // the same in the bin launch (positions + pad entries)
 
 // LDS view of a sort tile with one pad entry per 32 (256 B, one pass over the 64 banks):
 // the small-stride passes have lanes 16-32 B apart, which without padding land on 8 of the
@@ -650,13 +652,18 @@ struct SortBin {
   uint32_t n;
 };
 
-__device__ __forceinline__ uint2 bin_entry(const SortBin& b, uint32_t i) {
+__device__ __forceinline__ f2 bin_pos(const SortBin& b, uint32_t i) {
+  return reinterpret_cast<const f2*>(b.st)[2u * i];
+}
+__device__ __forceinline__ uint2 bin_key(const SortBin& b, f2 pos, uint32_t i) {
   const float r = b.cfg->smoothing_radius;
-  const f2 pos = reinterpret_cast<const f2*>(b.st)[2u * i];
   const int32_t cx = f32_to_i32((pos[0] + b.cfg->screen_bounds[1]) / r);
   const int32_t cy = f32_to_i32((pos[1] + b.cfg->screen_bounds[3]) / r);
   b.offsets[i] = 0xFFFFFFFFu;
   return make_uint2(cell_key(cx, cy, b.cfg->particle_count), i);
+}
+__device__ __forceinline__ uint2 bin_entry(const SortBin& b, uint32_t i) {
+  return bin_key(b, bin_pos(b, i), i);
 }
 
 // One register chunk of the passes of `stage` starting at `step` (sort_group: up to KMAX
@@ -717,8 +724,66 @@ __global__ __launch_bounds__(1024) void sph_sort_local_kernel(
   __shared__ uint2 lds[CAP + CAP / 32];
   const PaddedTile s{lds};
   const uint32_t base0 = blockIdx.x * tile;
-  if (vec) {  // two entries per lane: 16-B global loads (tile is even, base0 16-B aligned)
-    for (uint32_t q = 2u * threadIdx.x; q < tile; q += 2u * blockDim.x) {
+  if (!BIN && vec) {
+    // Two entries per lane in 16-B loads, all of a lane's loads issued before its first LDS
+    // write: a loop of load -> wait -> write paid one memory round trip per iteration.
+    // kSortLd loads per lane cover every (tile, threads) pair launch_sort_local uses
+    // (tile <= 16 x threads); the loop after it never runs for those.
+    uint4 v[kSortLd];
+#pragma unroll
+    for (uint32_t k = 0; k < kSortLd; ++k) {
+      const uint32_t q = 2u * threadIdx.x + k * 2u * blockDim.x;
+      if (q < tile) v[k] = *reinterpret_cast<const uint4*>(lookup + base0 + q);
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kSortLd; ++k) {
+      const uint32_t q = 2u * threadIdx.x + k * 2u * blockDim.x;
+      if (q < tile) {
+        s[q] = make_uint2(v[k].x, v[k].y);
+        s[q + 1u] = make_uint2(v[k].z, v[k].w);
+      }
+    }
+    for (uint32_t q = 2u * threadIdx.x + kSortLd * 2u * blockDim.x; q < tile; q += 2u * blockDim.x) {
+      const uint4 w = *reinterpret_cast<const uint4*>(lookup + base0 + q);
+      s[q] = make_uint2(w.x, w.y);
+      s[q + 1u] = make_uint2(w.z, w.w);
+    }
+  } else if (vec) {  // the bin launch: every position (or pad entry) load first, then the keys
+    // (kSortLdBin, not kSortLd: 8 would take the launch to 93 VGPRs, one 1024-thread block per CU)
+    f2 pa[kSortLdBin], pc[kSortLdBin];
+    uint4 lk[kSortLdBin];
+#pragma unroll
+    for (uint32_t k = 0; k < kSortLdBin; ++k) {
+      const uint32_t q = 2u * threadIdx.x + k * 2u * blockDim.x;
+      const uint32_t gq = base0 + q;
+      if (q < tile) {
+        if (gq < bin.n) {
+          pa[k] = bin_pos(bin, gq);
+          if (gq + 1u < bin.n) pc[k] = bin_pos(bin, gq + 1u);
+          else lk[k] = *reinterpret_cast<const uint4*>(lookup + gq);
+        } else {
+          lk[k] = *reinterpret_cast<const uint4*>(lookup + gq);
+        }
+      }
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kSortLdBin; ++k) {
+      const uint32_t q = 2u * threadIdx.x + k * 2u * blockDim.x;
+      const uint32_t gq = base0 + q;
+      if (q < tile) {
+        uint2 a, c;
+        if (gq < bin.n) {
+          a = bin_key(bin, pa[k], gq);
+          c = gq + 1u < bin.n ? bin_key(bin, pc[k], gq + 1u) : make_uint2(lk[k].z, lk[k].w);
+        } else {
+          a = make_uint2(lk[k].x, lk[k].y);
+          c = make_uint2(lk[k].z, lk[k].w);
+        }
+        s[q] = a;
+        s[q + 1u] = c;
+      }
+    }
+    for (uint32_t q = 2u * threadIdx.x + kSortLdBin * 2u * blockDim.x; q < tile; q += 2u * blockDim.x) {
       const uint32_t gq = base0 + q;
       uint2 a, c;
       if (BIN && gq < bin.n) {
@@ -795,10 +860,26 @@ __global__ __launch_bounds__(1024) void sph_sort_stage_kernel(uint2* __restrict_
     const uint32_t j = tau >> 5, c = (tau >> 4) & 1u, k = tau & 15u;
     return base + j * g + (c ? (g - 16u - r0 + k) : (r0 + k));
   };
-  for (uint32_t q = 2u * threadIdx.x; q < tile; q += 2u * blockDim.x) {  // 16-B aligned pairs
-    const uint4 v = *reinterpret_cast<const uint4*>(lookup + pos(q));
-    sm[q] = make_uint2(v.x, v.y);
-    sm[q + 1u] = make_uint2(v.z, v.w);
+  {  // 16-B aligned pairs, all of a lane's loads before its first LDS write (as in the local kernel)
+    uint4 v[kSortLd];
+#pragma unroll
+    for (uint32_t k = 0; k < kSortLd; ++k) {
+      const uint32_t q = 2u * threadIdx.x + k * 2u * blockDim.x;
+      if (q < tile) v[k] = *reinterpret_cast<const uint4*>(lookup + pos(q));
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kSortLd; ++k) {
+      const uint32_t q = 2u * threadIdx.x + k * 2u * blockDim.x;
+      if (q < tile) {
+        sm[q] = make_uint2(v[k].x, v[k].y);
+        sm[q + 1u] = make_uint2(v[k].z, v[k].w);
+      }
+    }
+    for (uint32_t q = 2u * threadIdx.x + kSortLd * 2u * blockDim.x; q < tile; q += 2u * blockDim.x) {
+      const uint4 w = *reinterpret_cast<const uint4*>(lookup + pos(q));
+      sm[q] = make_uint2(w.x, w.y);
+      sm[q + 1u] = make_uint2(w.z, w.w);
+    }
   }
   __syncthreads();
   for (uint32_t step = 0; step < T;) {
