@@ -196,8 +196,9 @@ int rps_create(const rps_create_info* info, rps_ctx** out);
 int rps_destroy(rps_ctx* ctx);
 const char* rps_last_error(const rps_ctx* ctx);
 
-/* == write_buffer(config, 144 B) (src/particle_buffers.rs:230-236): pinned staging +
- * hipMemcpyAsync into the device-resident config.  ext may be NULL (reference semantics:
+/* == write_buffer(config, 144 B) (src/particle_buffers.rs:230-236): the config is written
+ * into the device-resident copy by a kernel on the context stream (ordered before the next
+ * rps_step; the caller's struct may be reused at once).  ext may be NULL (reference semantics:
  * Euler, no attractors, no drag, no lifetime, shader_delay 5). */
 int rps_set_config(rps_ctx* ctx, const rps_config* cfg, const rps_ext_config* ext);
 int rps_get_config(const rps_ctx* ctx, rps_config* cfg, rps_ext_config* ext);

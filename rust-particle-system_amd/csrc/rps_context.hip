@@ -58,10 +58,8 @@ struct rps_ctx {
   float *ax = nullptr, *ay = nullptr;
   f2* nb_part = nullptr;  // N-body source-split partials (nb_splits x n float2)
   uint32_t nb_splits = 0;  // source splits of the force launch (RPS_NBODY_SPLITS overrides)
-  // device config (pinned upload)
+  // device config (rps_set_config writes it on the stream: config_store_kernel)
   rps_config* d_cfg = nullptr;
-  rps_config* h_cfg_pinned = nullptr;
-  hipEvent_t cfg_event = nullptr;
   // stats
   StatsPartial* partials = nullptr;
   uint32_t partial_cap = 0;
@@ -621,11 +619,6 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     ctx->err = "nbody pad launch failed";
     return bail(RPS_ERR_DEVICE);
   }
-  if (hipHostMalloc((void**)&ctx->h_cfg_pinned, sizeof(rps_config), hipHostMallocDefault) != hipSuccess ||
-      hipEventCreateWithFlags(&ctx->cfg_event, hipEventDisableTiming) != hipSuccess) {
-    ctx->err = "pinned config staging failed";
-    return bail(RPS_ERR_OUT_OF_MEMORY);
-  }
   if (hipStreamSynchronize(ctx->stream) != hipSuccess) {
     ctx->err = "hipStreamSynchronize failed";
     return bail(RPS_ERR_DEVICE);
@@ -641,8 +634,6 @@ int rps_destroy(rps_ctx* ctx) {
   if (ctx->comm) ncclCommDestroy(ctx->comm);
   for (auto ev : ctx->ev_start) (void)hipEventDestroy(ev);
   for (auto ev : ctx->ev_stop) (void)hipEventDestroy(ev);
-  if (ctx->cfg_event) (void)hipEventDestroy(ctx->cfg_event);
-  if (ctx->h_cfg_pinned) (void)hipHostFree(ctx->h_cfg_pinned);
   if (ctx->d_staging) (void)hipFree(ctx->d_staging);
   if (ctx->partials) (void)hipFree(ctx->partials);
   if (ctx->arena) (void)hipFree(ctx->arena);
@@ -674,13 +665,11 @@ int rps_set_config(rps_ctx* ctx, const rps_config* cfg, const rps_ext_config* ex
   ctx->cfg = *cfg;
   ctx->ext = e;
   ctx->have_config = true;
-  // write_buffer(config) (src/particle_buffers.rs:230-236): pinned staging -> device.  The
-  // staging slot is reused only after the previous copy has drained.
-  RPS_HIP(ctx, hipEventSynchronize(ctx->cfg_event));
-  std::memcpy(ctx->h_cfg_pinned, cfg, sizeof(rps_config));
-  RPS_HIP(ctx, hipMemcpyAsync(ctx->d_cfg, ctx->h_cfg_pinned, sizeof(rps_config),
-                              hipMemcpyHostToDevice, ctx->stream));
-  RPS_HIP(ctx, hipEventRecord(ctx->cfg_event, ctx->stream));
+  // write_buffer(config) (src/particle_buffers.rs:230-236): the 144 B ride in a one-wave
+  // kernel's arguments, ordered on the context stream before the next step's kernels.  A
+  // pinned-staging hipMemcpyAsync cost 12-18 us a frame at 65 536 particles (STREAM) and
+  // 35 us (SPH) against a kernel boundary (tools/config_upload_bench.py).
+  RPS_HIP(ctx, launch_config_store(*cfg, ctx->d_cfg, ctx->stream));
   return RPS_OK;
 }
 

@@ -32,6 +32,7 @@ hipError_t launch_stats_finalize(const StatsPartial* partials, uint32_t count,
 
 hipError_t launch_aos_to_soa(const rps_particle* aos, Fields f, Layout L, uint64_t offset,
                              uint64_t n, hipStream_t s);
+hipError_t launch_config_store(const rps_config& cfg, rps_config* dst, hipStream_t s);
 hipError_t launch_soa_to_aos(Fields f, Layout L, uint64_t offset, rps_particle* aos, uint64_t n,
                              float max_energy, int spawn_colour, hipStream_t s);
 hipError_t launch_field_gather(const float* field, Layout L, uint64_t offset, float* out,

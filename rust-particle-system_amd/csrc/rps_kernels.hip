@@ -452,6 +452,23 @@ __global__ __launch_bounds__(kBlock) void soa_to_aos_kernel(Fields f, Layout L, 
   *reinterpret_cast<f4*>(&aos[j].color[0]) = c;
 }
 
+// rps_set_config's upload: the 144-B config travels in this launch's kernarg segment and one
+// wave copies it to the device config, one dword per lane (ordered on the context stream
+// like any kernel; no staging buffer, no copy-engine handoff).
+struct ConfigStoreArgs {
+  rps_config cfg;
+  rps_config* dst;
+};
+__global__ __launch_bounds__(64) void config_store_kernel(ConfigStoreArgs a) {
+  typedef __attribute__((address_space(4))) const uint32_t* kword;
+  const uint32_t i = threadIdx.x;
+  if (i < sizeof(rps_config) / 4u) {
+    const kword src = (kword)((__attribute__((address_space(4))) const char*)__builtin_amdgcn_kernarg_segment_ptr() +
+                              offsetof(ConfigStoreArgs, cfg));
+    reinterpret_cast<uint32_t*>(a.dst)[i] = src[i];
+  }
+}
+
 // One field <-> a dense float range (checkpoint / SoA transfers through the layout).
 __global__ __launch_bounds__(kBlock) void field_gather_kernel(const float* field, Layout L,
                                                               uint64_t offset, float* out,
@@ -1407,6 +1424,14 @@ hipError_t launch_aos_to_soa(const rps_particle* aos, Fields f, Layout L, uint64
                              uint64_t n, hipStream_t s) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(aos_to_soa_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, s, aos, f, L, offset, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_config_store(const rps_config& cfg, rps_config* dst, hipStream_t s) {
+  ConfigStoreArgs a;
+  a.cfg = cfg;
+  a.dst = dst;
+  hipLaunchKernelGGL(config_store_kernel, dim3(1), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 
