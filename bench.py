@@ -65,6 +65,7 @@ def parse():
     ap.add_argument("--sph-cpu-n", type=int, default=1 << 22,
                     help="particles of the SPH CPU-baseline sample (oracle, OpenMP)")
     ap.add_argument("--sph-cpu-frames", type=int, default=3)
+    ap.add_argument("--no-configs", action="store_true", help="skip the C1/C2 side measurement")
     ap.add_argument("--export-reps", type=int, default=20,
                     help="render-interop export (rps_export_particles) repetitions timed on the headline state; 0: skip")
     ap.add_argument("--allpairs-timeout", type=float, default=240.0,
@@ -282,6 +283,35 @@ def allpairs_cpu_baseline(rps, args, ext):
     return {"value": float(n) * n * reps / el, "unit": "interactions/s", "cores": threads, "kind": "port",
             "sample": f"{n} x {n} interactions x {reps} (f32, oracle/rps_oracle.c orc_nbody_accel_f32_omp, "
                       f"-O3 -fopenmp omp simd, {threads} threads), {el:.1f} s; extrapolated to {args.allpairs_n}"}
+
+
+def configs_side(rps, args, d):
+    """BASELINE.json's other single-GPU streaming configs, measured beside the headline (each
+    rank its own replica; they are parity-test configs, and SURVEY 8(d) does not grade their
+    roofline: their state is a few MB to 32 MiB, cache-resident or launch-bound).  C1: 65 536
+    particles, one point attractor, Euler; C2: 2^20 particles, one attractor, velocity-Verlet.
+    Both with the reference's scatter and walls, every step active, 32 B/particle-step moved."""
+    out = {}
+    att = [dict(center=(0.0, 0.0), strength=1.0e5, softening=1.0)]
+    for key, n, integ, steps in (("c1", 65536, rps.EULER, 2000), ("c2", 1 << 20, rps.VERLET, 1000)):
+        cfg = rps.default_particle_config(n, gravity=9.8)
+        ext = rps.make_ext(integ, att, shader_delay=0)
+        ctx = rps.Context(n, rps.MODE_STREAM, device=d.local if d.dist else 0)
+        try:
+            ctx.set_config(cfg, ext)
+            ctx.upload(rps.setup_particles_scatter(cfg, n, seed=args.seed))
+            ctx.step(100)
+            ctx.sync()
+            t0 = time.perf_counter()
+            gpu_ms = ctx.time_steps(steps)
+            wall = time.perf_counter() - t0
+        finally:
+            ctx.close()
+        out[key] = {"particles": n, "integrator": "euler" if integ == rps.EULER else "verlet", "attractors": 1,
+                    "steps": steps, "us_per_step": gpu_ms * 1e3 / steps, "wall_us_per_step": wall * 1e6 / steps,
+                    "updates_per_s": n * steps / (gpu_ms * 1e-3),
+                    "moved_gbps": 32.0 * n * steps / (gpu_ms * 1e-3) / 1e9}
+    return out
 
 
 def sph_side(rps, args, d):
@@ -504,7 +534,8 @@ def main():
         line["export"] = export
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(rps, args, cfg, ext)
-    sides = [("sph", sph_side, args.sph_n > 0), ("allpairs", allpairs, args.allpairs_n > 0)]
+    sides = [("configs", configs_side, not args.no_configs), ("sph", sph_side, args.sph_n > 0),
+             ("allpairs", allpairs, args.allpairs_n > 0)]
     for key, fn, on in sides:
         if not on:
             continue

@@ -11,7 +11,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BENCH = os.path.join(ROOT, "bench.py")
-ARGS = ["--steps", "20", "--warmup", "2", "--particles", "4096", "--no-cpu-baseline", "--sph-n", "0"]
+ARGS = ["--steps", "20", "--warmup", "2", "--particles", "4096", "--no-cpu-baseline", "--sph-n", "0", "--no-configs"]
 
 
 def _run(extra, env_extra=None, timeout=240):
