@@ -177,11 +177,12 @@ def _abs_sum_targets(ext, tx, ty, sx, sy):
     return out * float(ext.nbody_strength)
 
 
-@pytest.mark.parametrize("splits", [None, "1"])
-def test_nbody_full_size(gpu, orc, monkeypatch, splits):
+@pytest.mark.parametrize("n,splits", [(1 << 22, None), (1 << 22, "1"), (1 << 24, None)])
+def test_nbody_full_size(gpu, orc, monkeypatch, n, splits):
     """2^22 targets over 2^22 sources -- the bench's `allpairs` step: the default source
     splits (12 at this size) and one forced split (the kernel writes G*a directly, the
-    variant launches with >= 24576 target blocks run).  Four chunks of 16 contiguous
+    variant launches with >= 24576 target blocks run) -- and BASELINE.json's C4 config, 2^24
+    over 2^24 (one split; one step is ~45 s on one MI355X).  Four chunks of 16 contiguous
     targets spread over the array (first block, middle, the last block's tail) are checked
     against the oracle's f64 direct sum over every source, with the same bound as the small
     tests (the two-level summation keeps the error near 1e-6 of |a| at this size); the
@@ -189,7 +190,6 @@ def test_nbody_full_size(gpu, orc, monkeypatch, splits):
     if splits:
         monkeypatch.setenv("RPS_NBODY_SPLITS", splits)
     rps = gpu
-    n = 1 << 22
     cfg = config_c1(rps, n)
     ext = rps.make_ext(nbody_strength=1.0e3, nbody_softening=1.0, shader_delay=0)
     g = np.random.default_rng(2024)
