@@ -1680,11 +1680,13 @@ hipError_t launch_sph_offsets(const SphBuffers& b, hipStream_t s) {
 // (SphBuffers::batch_d / batch_s, from RPS_SPH_BATCH[_D|_S] at rps_create): by size, measured
 // (DESIGN.md §5).
 int sph_batch(bool density, uint32_t p, int forced) {
-  if (forced == 4 || forced == 8 || forced == 16) return forced;
+  if (forced == 4 || forced == 6 || forced == 8 || forced == 16) return forced;
   // The sim scan keeps 4 entries in flight up to P = 2^21, where its slot records stay in
-  // the caches (2^20 frame 0.404 -> 0.392 ms, 2^21 0.670 -> 0.651), and 8 beyond (2^22: 1.25
-  // vs 1.28 ms with 4).  The density scan is indifferent (4 or 8 within 0.3 %).
-  return density || p > (1u << 21) ? 8 : 4;
+  // the caches (2^20 frame 0.404 -> 0.392 ms, 2^21 0.670 -> 0.651), and 6 beyond (2^22: 1.2223
+  // ms with 8, 1.2129 with 6 -- 91 VGPRs, 5 waves/SIMD instead of 111 and 4 --, 1.28 with 4,
+  // 1.2989 with 12).  The density scan is indifferent (4 or 8 within 0.3 %) and keeps 8.
+  if (density) return 8;
+  return p > (1u << 21) ? 6 : 4;
 }
 
 bool sph_fold_offsets() {
@@ -1731,6 +1733,7 @@ hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s) {
                        b.cfg, b.offsets, b.ends, b.sl, b.st, b.p)
   switch (sph_batch(false, b.p, b.batch_s)) {
     case 4: RPS_SIM(4); break;
+    case 6: RPS_SIM(6); break;
     case 16: RPS_SIM(16); break;
     default: RPS_SIM(8); break;
   }

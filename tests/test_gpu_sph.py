@@ -156,11 +156,11 @@ def test_sph_large_frames_bitwise(gpu, orc, n):
 
 
 @pytest.mark.parametrize("n", [65536, 50000])
-@pytest.mark.parametrize("batch", [("RPS_SPH_BATCH_S", "8"), ("RPS_SPH_BATCH_S", "16"),
+@pytest.mark.parametrize("batch", [("RPS_SPH_BATCH_S", "6"), ("RPS_SPH_BATCH_S", "8"), ("RPS_SPH_BATCH_S", "16"),
                                    ("RPS_SPH_BATCH_D", "4"), ("RPS_SPH_BATCH_D", "16")])
 def test_sph_forced_scan_batches(gpu, orc, monkeypatch, n, batch):
     """Every scan-batch variant of the density and sim kernels, forced per context at small N
-    (the default picks the sim batch 8 only above P = 2^21): P = N (slot self-skip) and
+    (the default picks the sim batch 6 only above P = 2^21): P = N (slot self-skip) and
     N = 50 000 (pads, index self-skip), every pass bitwise over 3 frames."""
     rps = gpu
     monkeypatch.setenv(*batch)
@@ -172,7 +172,7 @@ def test_sph_forced_scan_batches(gpu, orc, monkeypatch, n, batch):
 def test_sph_bench_workload_full_size(gpu, orc, n):
     """The bench's `sph` workload exactly (2^22): particles of the reference scatter over a
     viewport scaled to the default density, every frame active.  P > 2^21 selects the sim
-    scan's 8-entry batch, 8192-entry sort tiles with 3 passes per register chunk and the
+    scan's 6-entry batch, 8192-entry sort tiles with 3 passes per register chunk and the
     five-pass register-fused global stage; at P = 2^21 (the largest size on the 4-entry sim
     batch) that stage is a gathered-tile launch.  Two frames, every pass bitwise."""
     rps = gpu
