@@ -60,6 +60,34 @@ def test_nbody_accel_and_integrate(gpu, orc, n):
     assert_soa_bitwise(got, ref)
 
 
+@pytest.mark.parametrize("n", [1, 2, 3, 5])
+def test_nbody_tiny(gpu, orc, n):
+    """Tiny N (one partial tile, mostly far-away pads): a lone particle feels exactly no
+    force (its self term has dx = 0 and every pad adds +0); a few particles match the oracle
+    within the tolerance; integration bitwise."""
+    rps = gpu
+    cfg = config_c1(rps, n, gravity=3.0)
+    ext = rps.make_ext(nbody_strength=50.0, nbody_softening=2.0, shader_delay=0)
+    g = np.random.default_rng(100 + n)
+    soa = dict(x=g.uniform(-90, 90, n).astype(F), y=g.uniform(-50, 50, n).astype(F),
+               vx=g.normal(0, 10, n).astype(F), vy=g.normal(0, 10, n).astype(F))
+    with rps.Context(n, rps.MODE_NBODY) as ctx:
+        ctx.set_config(cfg, ext)
+        ctx.upload_soa(soa)
+        ctx.step(1)
+        ax = ctx.read_debug(rps.DEBUG_ACCEL_X)
+        ay = ctx.read_debug(rps.DEBUG_ACCEL_Y)
+        got = ctx.download_soa()
+    if n == 1:
+        assert ax[0] == 0.0 and ay[0] == 0.0
+    else:
+        rx, ry = orc.nbody_accel(ext, soa["x"], soa["y"])
+        _check_accel(ax, ay, rx, ry, ext, soa["x"], soa["y"])
+    ref = copy_soa(soa)
+    orc.nbody_integrate(cfg, ext, ax, ay, ref)
+    assert_soa_bitwise(got, ref)
+
+
 def test_nbody_requires_softening(gpu):
     rps = gpu
     with rps.Context(256, rps.MODE_NBODY) as ctx:
