@@ -52,6 +52,9 @@ struct rps_ctx {
   uint32_t P = 0;
   uint32_t sort_passes = 0, sort_launches = 0;
   uint8_t sph_batch_d = 0, sph_batch_s = 0;  // forced scan batches (0: by size)
+  SphLayoutArgs lay{};     // spatial record layout (P == N, RPS_SPH_LAYOUT != 0): arrays
+  uint32_t cell_cap = 0;   // their cell capacity (0: no layout)
+  bool layout_last = false;  // the last active frame used the layout (slot records in storage order)
   // N-body
   f2* pos_all = nullptr;
   uint64_t ns_padded = 0;
@@ -287,6 +290,9 @@ SphBuffers sph_buffers(rps_ctx* ctx) {
   b.p = ctx->P;
   b.batch_d = ctx->sph_batch_d;
   b.batch_s = ctx->sph_batch_s;
+  b.lay = ctx->lay;
+  b.cell_cap = ctx->cell_cap;
+  b.layout = ctx->layout_last;
   return b;
 }
 
@@ -438,9 +444,14 @@ int step_sph_grid(rps_ctx* ctx, bool fold_offsets) {
   return RPS_OK;
 }
 
-int step_sph_sim(rps_ctx* ctx, bool with_offsets) {
+int step_sph_sim(rps_ctx* ctx, bool with_offsets, bool layout, const SphGrid& g) {
+  ctx->layout_last = layout;
   SphBuffers b = sph_buffers(ctx);
-  RPS_HIP(ctx, launch_sph_pre(b, ctx->stream, with_offsets));
+  b.lay.g = g;
+  if (layout)
+    RPS_HIP(ctx, launch_sph_layout_pre(b, ctx->stream));
+  else
+    RPS_HIP(ctx, launch_sph_pre(b, ctx->stream, with_offsets));
   int rc = prof_begin(ctx);
   if (rc) return rc;
   RPS_HIP(ctx, launch_sph_sim(b, ctx->stream));
@@ -569,6 +580,21 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     slots.push_back({(void**)&ctx->offsets, align_up(n * sizeof(uint32_t), 256)});
     slots.push_back({(void**)&ctx->dens, align_up(n * sizeof(f2), 256)});
     slots.push_back({(void**)&ctx->pred, align_up(n * sizeof(f2), 256)});
+    // Spatial record layout (rps_kernels.hip): RPS_SPH_LAYOUT=0 off, 1 (default) from 2^21
+    // particles, where it is measured faster (2^22 frame 1.212 -> 1.121 ms, 2^21 0.633 ->
+    // 0.609; 2^20 0.385 -> 0.391 and 2^18 0.166 -> 0.176 slower: DESIGN.md §5), 2 at any P == N.
+    const int lay_mode = env_int("RPS_SPH_LAYOUT", 1);
+    if (P == n && (lay_mode == 2 || (lay_mode == 1 && n >= (1u << 21)))) {
+      // Up to 2 cells per particle (the bench's viewport has ~0.5).
+      ctx->cell_cap = (uint32_t)std::max<size_t>(2 * n, 4096);
+      const size_t cap = ctx->cell_cap;
+      slots.push_back({(void**)&ctx->lay.cell_info, align_up(cap * sizeof(uint2), 256)});
+      slots.push_back({(void**)&ctx->lay.cellrun, align_up(cap * sizeof(uint2), 256)});
+      slots.push_back({(void**)&ctx->lay.run2, align_up(n * sizeof(uint2), 256)});
+      slots.push_back({(void**)&ctx->lay.part, align_up((cap / 256 + 1) * sizeof(uint32_t), 256)});
+      slots.push_back({(void**)&ctx->lay.out_keys, align_up(n * sizeof(uint32_t), 256)});
+      slots.push_back({(void**)&ctx->lay.n_out, 256});
+    }
   }
   if (ctx->mode == RPS_MODE_NBODY) {
     ctx->ns_padded = (global + kNbodyTile - 1) / kNbodyTile * kNbodyTile;
@@ -849,6 +875,10 @@ int rps_read_debug(rps_ctx* ctx, int which, void* dst, uint64_t bytes) {
   }
   if (which == RPS_DEBUG_DENSITIES || which == RPS_DEBUG_PREDICTED)
     RPS_HIP(ctx, launch_sph_debug_views(sph_buffers(ctx), ctx->stream));
+  // A spatial-layout frame measures its runs without writing the reference's offsets (the bin
+  // pass reset them): pass 3 (wgsl:507-525) on the frame's sorted lookup, on demand.
+  if (which == RPS_DEBUG_LOOKUP_OFFSETS && ctx->layout_last)
+    RPS_HIP(ctx, launch_sph_offsets(sph_buffers(ctx), ctx->stream));
   RPS_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
   RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return RPS_OK;
@@ -900,9 +930,12 @@ int rps_step(rps_ctx* ctx, uint32_t nsteps) {
   for (uint32_t s = 0; s < nsteps; ++s) {
     ctx->cfg.frame_count += 1;  // src/particle_buffers.rs:227
     const bool active = ctx->cfg.frame_count >= ctx->ext.shader_delay;  // wgsl:426, :442
+    SphGrid grid{};
+    const bool layout = ctx->mode == RPS_MODE_SPH && active && sph_layout_grid(ctx->cfg, ctx->cell_cap, &grid);
     if (ctx->mode == RPS_MODE_SPH) {
-      // passes 1-3 run every frame (particle_compute.rs:105-163)
-      rc = step_sph_grid(ctx, active && sph_fold_offsets());
+      // passes 1-3 run every frame (particle_compute.rs:105-163); on an active frame the
+      // offsets pass rides in the next kernel (the layout's runs kernel or predict)
+      rc = step_sph_grid(ctx, active && (layout || sph_fold_offsets()));
       if (rc) return rc;
     }
     if (!active) continue;
@@ -927,7 +960,7 @@ int rps_step(rps_ctx* ctx, uint32_t nsteps) {
     switch (ctx->mode) {
       case RPS_MODE_STREAM: rc = step_stream(ctx); break;
       case RPS_MODE_NBODY: rc = step_nbody(ctx); break;
-      default: rc = step_sph_sim(ctx, sph_fold_offsets()); break;
+      default: rc = step_sph_sim(ctx, sph_fold_offsets(), layout, grid); break;
     }
     if (rc) return rc;
     ++ctx->active_steps;

@@ -104,6 +104,21 @@ struct SphSlots {
   f2* cur_s;     // P current positions (Euler base)
   uint64_t* nbr_mask;  // 2 x P: bit f set <=> flat entry f of the nine runs is within the radius
 };
+// Cell range of the spatial record layout (rps_kernels.hip): cells [cx_lo, cx_lo + w) x
+// [cy_lo, cy_lo + h), enumerated in 8 x 8 tiles, tw tiles per row; cells = tiles x 64.
+struct SphGrid {
+  int32_t cx_lo, cy_lo;
+  uint32_t w, h, tw, cells;
+};
+struct SphLayoutArgs {
+  SphGrid g;
+  uint2* cell_info;    // cells: {first slot, length} of the run a cell owns ({0, 0}: none)
+  uint2* cellrun;      // cells: storage {start, end} of the cell's key's run (start >= N: none)
+  uint2* run2;         // N: storage {start, end} per key ({0xFFFFFFFF, 0}: none; reset in bin)
+  uint32_t* part;      // cells / 256 + 1: 256-cell block sums -> bases (0 between frames)
+  uint32_t* out_keys;  // N: keys of runs placed after the grid's
+  uint32_t* n_out;     // 1: their count (0 between frames)
+};
 struct SphBuffers {
   const rps_config* cfg;  // device-resident ParticleConfig
   f4* st;            // N packed {x, y, vx, vy}: read by bin/predict, written in place by the sim
@@ -117,7 +132,15 @@ struct SphBuffers {
   uint32_t p;        // next_pow2(N)
   uint8_t batch_d;   // scan entries in flight per lane, density / sim pass (4, 8, 16;
   uint8_t batch_s;   //   0: by size, sph_batch); per context, RPS_SPH_BATCH[_D|_S] at create
+  bool layout;       // this frame uses the spatial record layout (lay.* valid, P == N)
+  uint32_t cell_cap; // capacity of lay.cell_info / cellrun (0: layout never available)
+  SphLayoutArgs lay;
 };
+// The layout's cell range for `c` if it fits `cell_cap` cells (false: frame without layout).
+bool sph_layout_grid(const rps_config& c, uint32_t cell_cap, SphGrid* g);
+// Active-frame passes 3-4 with the spatial layout: runs, count, scan, write + predict,
+// fixup, density.
+hipError_t launch_sph_layout_pre(const SphBuffers& b, hipStream_t s);
 // Scan batch of the density (`density`) or sim pass at P entries; `forced` != 0 wins.
 int sph_batch(bool density, uint32_t p, int forced);
 // Runs the whole bitonic network of src/particle_compute.rs:117-149; returns the number of

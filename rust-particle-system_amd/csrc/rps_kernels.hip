@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 
 #include "rps_internal.hpp"
@@ -667,6 +668,7 @@ struct SortBin {
   const f4* st;  // packed {x, y, vx, vy} per particle
   uint32_t* offsets;
   uint32_t n;
+  uint2* run2;  // spatial layout's storage runs, reset with offsets (nullptr: no layout)
 };
 
 __device__ __forceinline__ f2 bin_pos(const SortBin& b, uint32_t i) {
@@ -677,6 +679,7 @@ __device__ __forceinline__ uint2 bin_key(const SortBin& b, f2 pos, uint32_t i) {
   const int32_t cx = f32_to_i32((pos[0] + b.cfg->screen_bounds[1]) / r);
   const int32_t cy = f32_to_i32((pos[1] + b.cfg->screen_bounds[3]) / r);
   b.offsets[i] = 0xFFFFFFFFu;
+  if (b.run2) b.run2[i] = make_uint2(0xFFFFFFFFu, 0u);
   return make_uint2(cell_key(cx, cy, b.cfg->particle_count), i);
 }
 __device__ __forceinline__ uint2 bin_entry(const SortBin& b, uint32_t i) {
@@ -928,6 +931,41 @@ __global__ __launch_bounds__(kBlock) void sph_offsets_kernel(const uint2* __rest
   if (key != next || i + 1u == n) ends[key] = i + 1u;
 }
 
+// Spatial record layout: cell enumeration (8 x 8 tiles; see the layout kernels below).
+constexpr uint32_t kCellOut = 0xFFFFFFFFu;
+constexpr uint32_t kCellPending = 0xFFFFFFFEu;  // cellrun entry to resolve through run2
+constexpr uint32_t kRunScan = 32u;               // longest run a runs-kernel lane measures itself
+
+__device__ __forceinline__ uint32_t grid_enum_xy(const SphGrid& g, uint32_t x, uint32_t y) {
+  return (((y >> 3) * g.tw + (x >> 3)) << 6) | ((y & 7u) << 3) | (x & 7u);
+}
+__device__ __forceinline__ uint32_t grid_enum(const SphGrid& g, int32_t cx, int32_t cy) {
+  const uint32_t x = (uint32_t)cx - (uint32_t)g.cx_lo, y = (uint32_t)cy - (uint32_t)g.cy_lo;
+  if (x >= g.w || y >= g.h) return kCellOut;
+  return grid_enum_xy(g, x, y);
+}
+
+// Inverse of grid_enum; false for the padding cells of edge tiles.
+__device__ __forceinline__ bool grid_cell(const SphGrid& g, uint32_t e, int32_t& cx, int32_t& cy) {
+  const uint32_t tile = e >> 6;
+  const uint32_t ty = tile / g.tw;
+  const uint32_t x = (tile - ty * g.tw) * 8u + (e & 7u), y = ty * 8u + ((e >> 3) & 7u);
+  cx = (int32_t)((uint32_t)g.cx_lo + x);
+  cy = (int32_t)((uint32_t)g.cy_lo + y);
+  return x < g.w && y < g.h;
+}
+
+// Workgroup -> chunk of the launch's index range.  xcd != 0: workgroups are dealt round-robin
+// over the 8 XCDs (MI355X_MICROARCH.md, dispatch), so workgroup b takes chunk
+// (b % 8) * (nb / 8) + ...: each XCD walks one contiguous eighth of the range, and with the
+// spatial record layout one spatial band whose records stay in that XCD's L2.
+__device__ __forceinline__ uint32_t wg_index(uint32_t xcd) {
+  const uint32_t b = blockIdx.x;
+  if (!xcd) return b;
+  const uint32_t nb = gridDim.x, x = b & 7u, q = nb >> 3, r = nb & 7u;
+  return x * q + min(x, r) + (b >> 3);
+}
+
 __constant__ int32_t kGridOff[9][2] = {{-1, -1}, {-1, 0}, {-1, 1}, {0, -1}, {0, 0},
                                        {0, 1},   {1, -1}, {1, 0},  {1, 1}};
 
@@ -939,6 +977,20 @@ __constant__ int32_t kGridOff[9][2] = {{-1, -1}, {-1, 0}, {-1, 1}, {0, -1}, {0, 
 // densities buffers are not written on the hot path; launch_sph_debug_views rebuilds them
 // from the slot records on readback.  Pad slots repeat some particle and
 // write identical values.
+// apply_gravity (wgsl:397-400) and the prediction (:402-405) of particle i into slot u.
+__device__ __forceinline__ void predict_slot(const rps_config* __restrict__ cfg, const f4* __restrict__ st,
+                                             const SphSlots& sl, uint32_t u, uint32_t i) {
+  const f4 s = st[i];
+  const float dt = cfg->fixed_delta_time;
+  const float qx = s[2] + 0.0f * dt;  // apply_gravity, wgsl:397-400
+  const float qy = s[3] + (-cfg->gravity) * dt;
+  const float px = s[0] + qx * dt, py = s[1] + qy * dt;  // wgsl:402-405
+  sl.pp_s[u] = f2{px, py};
+  sl.rec_pv[u] = f4{px, py, qx, qy};
+  sl.idx_s[u] = i;
+  sl.cur_s[u] = f2{s[0], s[1]};
+}
+
 __global__ __launch_bounds__(kBlock) void sph_predict_kernel(const rps_config* __restrict__ cfg,
                                                              const uint2* __restrict__ lookup,
                                                              const f4* __restrict__ st,
@@ -955,16 +1007,7 @@ __global__ __launch_bounds__(kBlock) void sph_predict_kernel(const rps_config* _
     if (e.x != prev) offsets[e.x] = t;
     if (e.x != next || t + 1u == n_offsets) ends[e.x] = t + 1u;
   }
-  const uint32_t i = e.y;
-  const f4 s = st[i];
-  const float dt = cfg->fixed_delta_time;
-  const float qx = s[2] + 0.0f * dt;  // apply_gravity, wgsl:397-400
-  const float qy = s[3] + (-cfg->gravity) * dt;
-  const float px = s[0] + qx * dt, py = s[1] + qy * dt;  // wgsl:402-405
-  sl.pp_s[t] = f2{px, py};
-  sl.rec_pv[t] = f4{px, py, qx, qy};
-  sl.idx_s[t] = i;
-  sl.cur_s[t] = f2{s[0], s[1]};
+  predict_slot(cfg, st, sl, t, e.y);
 }
 
 // The nine runs a particle at predicted position p scans, in the reference's cell order
@@ -980,19 +1023,53 @@ __device__ __forceinline__ uint32_t grid_key(int32_t cx, int32_t cy, int o, uint
                   (int32_t)((uint32_t)cy + (uint32_t)kGridOff[o][1]), N);
 }
 
-__device__ __forceinline__ uint32_t nine_runs(const uint32_t* __restrict__ offsets,
-                                              const uint32_t* __restrict__ ends, float px, float py,
-                                              float xoff, float yoff, float r, uint32_t N,
-                                              RunTable& runs) {
+// Where a scan finds the run of a neighbour cell: key-indexed {offsets, ends} in lookup order,
+// or (spatial layout) the cell-ordered storage runs, with the key-indexed run2 for lanes whose
+// 3 x 3 block leaves the layout's grid.
+struct RunBounds {
+  const uint32_t* offsets;
+  const uint32_t* ends;
+  const uint2* cellrun;
+  const uint2* run2;
+  SphGrid g;
+};
+
+template <bool LAYOUT>
+__device__ __forceinline__ uint32_t nine_runs(const RunBounds& rb, float px, float py, float xoff,
+                                              float yoff, float r, uint32_t N, RunTable& runs) {
   const int32_t cx = f32_to_i32((px + xoff) / r);  // particle_position_to_cell_coord, wgsl:121-130
   const int32_t cy = f32_to_i32((py + yoff) / r);
-  uint32_t key[9], s[9], e[9];
+  uint32_t s[9], e[9];
+  if (LAYOUT) {
+    const uint32_t x = (uint32_t)cx - (uint32_t)rb.g.cx_lo, y = (uint32_t)cy - (uint32_t)rb.g.cy_lo;
+    const bool in = x - 1u < rb.g.w - 2u && y - 1u < rb.g.h - 2u;  // all nine cells in the grid
+    if (!__builtin_amdgcn_ballot_w64(!in)) {
 #pragma unroll
-  for (int o = 0; o < 9; ++o) key[o] = grid_key(cx, cy, o, N);
+      for (int o = 0; o < 9; ++o) {
+        const uint2 v = rb.cellrun[grid_enum_xy(rb.g, x + (uint32_t)kGridOff[o][0], y + (uint32_t)kGridOff[o][1])];
+        s[o] = v.x;
+        e[o] = v.y;
+      }
+    } else {
 #pragma unroll
-  for (int o = 0; o < 9; ++o) {
-    s[o] = offsets[key[o]];
-    e[o] = ends[key[o]];
+      for (int o = 0; o < 9; ++o) {
+        const uint2* q = in ? rb.cellrun + grid_enum_xy(rb.g, x + (uint32_t)kGridOff[o][0],
+                                                        y + (uint32_t)kGridOff[o][1])
+                            : rb.run2 + grid_key(cx, cy, o, N);
+        const uint2 v = *q;
+        s[o] = v.x;
+        e[o] = v.y;
+      }
+    }
+  } else {
+    uint32_t key[9];
+#pragma unroll
+    for (int o = 0; o < 9; ++o) key[o] = grid_key(cx, cy, o, N);
+#pragma unroll
+    for (int o = 0; o < 9; ++o) {
+      s[o] = rb.offsets[key[o]];
+      e[o] = rb.ends[key[o]];
+    }
   }
   uint32_t c = 0, m = 0;
 #pragma unroll
@@ -1041,19 +1118,18 @@ struct RunCursor {
 //
 // calculate_density, compute_shader.wgsl:207-254: entries summed in run order, kScanBatch
 // predicted positions in flight per lane across run boundaries.
-template <int kScanBatch>
+template <int kScanBatch, bool LAYOUT>
 __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* __restrict__ cfg,
-                                                             const uint32_t* __restrict__ offsets,
-                                                             const uint32_t* __restrict__ ends,
-                                                             SphSlots sl, uint32_t p_slots) {
-  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+                                                             RunBounds rb, SphSlots sl, uint32_t p_slots,
+                                                             uint32_t xcd) {
+  const uint32_t t = wg_index(xcd) * kBlock + threadIdx.x;
   if (t >= p_slots) return;
   const f2 p = sl.pp_s[t];
   const float r = cfg->smoothing_radius, r2 = r * r;
   const uint32_t N = cfg->particle_count;
   const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
   __shared__ RunTable runs;
-  const uint32_t total = nine_runs(offsets, ends, p[0], p[1], cfg->screen_bounds[1],
+  const uint32_t total = nine_runs<LAYOUT>(rb, p[0], p[1], cfg->screen_bounds[1],
                                    cfg->screen_bounds[3], r, N, runs);
   RunCursor rc(runs);
   float d = 0.0f, nd = 0.0f;
@@ -1171,13 +1247,11 @@ __device__ __forceinline__ void scan_runs(const SphSlots& sl, const RunTable& ru
 // buffer does; a second one (ping-pong) only added 64 MB at 2^22 to the frame's working set,
 // which is what decides whether the scattered 16-B writes merge in the Infinity Cache or go
 // to HBM as partial-line writes.
-template <int kScanBatch, bool kPads>
+template <int kScanBatch, bool kPads, bool LAYOUT>
 __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __restrict__ cfg,
-                                                         const uint32_t* __restrict__ offsets,
-                                                         const uint32_t* __restrict__ ends,
-                                                         SphSlots sl, f4* __restrict__ st,
-                                                         uint32_t p_slots) {
-  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+                                                         RunBounds rb, SphSlots sl, f4* __restrict__ st,
+                                                         uint32_t p_slots, uint32_t xcd) {
+  const uint32_t t = wg_index(xcd) * kBlock + threadIdx.x;
   if (t >= p_slots) return;
   const f4 own = sl.rec_pd[t];  // own predicted position (xy) and P / rho^2 (z)
   const f2 own_d = sl.dens_s[t];
@@ -1194,7 +1268,7 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
   const float P_rho2 = own[2];             // loop-invariant halves of pressure_term and
   const float Pn_rho2 = Pn / (rho * rho);  // near_pressure_term (wgsl:323-327)
   __shared__ RunTable runs;
-  const uint32_t total = nine_runs(offsets, ends, p[0], p[1], cfg->screen_bounds[1],
+  const uint32_t total = nine_runs<LAYOUT>(rb, p[0], p[1], cfg->screen_bounds[1],
                                    cfg->screen_bounds[3], r, N, runs);
   const bool masked = total <= 128u;
   const uint64_t m0 = masked ? sl.nbr_mask[t] : 0u, m1 = masked ? sl.nbr_mask[p_slots + t] : 0u;
@@ -1277,6 +1351,7 @@ __global__ __launch_bounds__(kBlock) void sph_debug_views_kernel(SphSlots sl, f2
 __global__ __launch_bounds__(kBlock) void sph_count_kernel(const rps_config* __restrict__ cfg,
                                                            const uint32_t* __restrict__ offsets,
                                                            const uint32_t* __restrict__ ends,
+                                                           const uint2* __restrict__ run2,
                                                            const f2* __restrict__ pp_s,
                                                            uint32_t p_slots,
                                                            unsigned long long* __restrict__ out) {
@@ -1290,9 +1365,9 @@ __global__ __launch_bounds__(kBlock) void sph_count_kernel(const rps_config* __r
     const int32_t cy = f32_to_i32((p[1] + cfg->screen_bounds[3]) / r);
     for (int o = 0; o < 9; ++o) {
       const uint32_t key = grid_key(cx, cy, o, N);
-      const uint32_t s0 = offsets[key];
+      const uint32_t s0 = run2 ? run2[key].x : offsets[key];  // storage runs with the layout
       if (s0 >= N) continue;
-      const uint32_t e0 = ends[key];
+      const uint32_t e0 = run2 ? run2[key].y : ends[key];
       scanned += e0 - s0;
       for (uint32_t j = s0; j < e0; ++j) {
         const f2 q = pp_s[j];
@@ -1316,6 +1391,174 @@ __global__ __launch_bounds__(kBlock) void sph_count_kernel(const rps_config* __r
     unsigned long long v = 0;
     for (uint32_t w = 0; w < kBlock / 64; ++w) v += part[threadIdx.x][w];
     out[2ull * blockIdx.x + threadIdx.x] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Spatial record layout (P == N; DESIGN.md §5 "Record layout").  The slot records are stored
+// run by run in a spatial order of the cells instead of the sorted lookup's hash order: a
+// key's run (its entries in lookup order) stays contiguous and in order, so every scan visits
+// the same entries in the same order as the reference (bitwise), but the runs of neighbouring
+// cells sit next to each other, and a cell-ordered table of storage runs (cellrun) replaces
+// the scans' key-indexed (hash-random) run bounds:
+//   runs kernel (slot order): offsets/ends as the reference's pass 3; at a run start, the
+//       run's length and the cell of its first particle (its owner): cell_info[cell] =
+//       {first slot, length}, and the length added to the owner's 256-cell block sum;
+//       runs whose first particle lies outside the grid (or longer than kRunScan) go to a list;
+//   scan (one workgroup): block bases; the listed runs placed after the grid's;
+//   write (cell order): each owned run gets the next storage range -> run2[key], cellrun[cell],
+//       and its lookup entries are copied to lookup2 (storage order); cells owning no run
+//       are marked, and the predict pass resolves them through run2 (a key shared by several
+//       cells belongs to one of them).
+// Cells are enumerated in 8 x 8 tiles, tiles row-major over the screen's cell range.
+// Exclusive prefix of v over a workgroup of NT threads; *total = the workgroup's sum.
+template <uint32_t NT>
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* total) {
+  __shared__ uint32_t wsum[NT / 64];
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  if (lane == 63u) wsum[wave] = x;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < NT / 64; ++w) {
+    const uint32_t s = wsum[w];
+    pre += w < wave ? s : 0u;
+    tot += s;
+  }
+  __syncthreads();
+  *total = tot;
+  return pre + x - v;
+}
+
+// Each run's length and owner cell (the layout's replacement for pass 3: the scans find runs
+// through cellrun / run2, and the reference's offsets are rebuilt on debug readback).
+__global__ __launch_bounds__(kBlock) void sph_runs_kernel(SphLayoutArgs a, const rps_config* __restrict__ cfg,
+                                                          const uint2* __restrict__ lookup,
+                                                          const f4* __restrict__ st, uint32_t n) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= n) return;
+  const uint2 e = lookup[t];
+  const uint32_t prev = t > 0u ? lookup[t - 1u].x : 0xFFFFFFFFu;
+  if (e.x == prev) return;
+  // The cell of the run's first particle, computed as the bin pass did (same state, same
+  // ops), so its key is e.x; anything else (never seen) is handled as outside the grid.
+  const f4 s = st[e.y];
+  uint32_t len = 1;
+  while (len <= kRunScan && t + len < n && lookup[t + len].x == e.x) ++len;
+  const float r = cfg->smoothing_radius;
+  const int32_t cx = f32_to_i32((s[0] + cfg->screen_bounds[1]) / r);
+  const int32_t cy = f32_to_i32((s[1] + cfg->screen_bounds[3]) / r);
+  const uint32_t c = cell_key(cx, cy, cfg->particle_count) == e.x ? grid_enum(a.g, cx, cy) : kCellOut;
+  if (c == kCellOut || len > kRunScan)
+    a.out_keys[atomicAdd(a.n_out, 1u)] = t;  // placed by the scan kernel
+  else
+    a.cell_info[c] = make_uint2(t, len);
+}
+
+// Run lengths owned by each 256-cell block.
+__global__ __launch_bounds__(kBlock) void sph_layout_count_kernel(SphLayoutArgs a) {
+  const uint32_t e = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t len = e < a.g.cells ? a.cell_info[e].y : 0u;
+  uint32_t tot;
+  block_exclusive_scan<kBlock>(len, &tot);
+  if (threadIdx.x == 0) a.part[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(1024) void sph_layout_scan_kernel(SphLayoutArgs a,
+                                                               const rps_config* __restrict__ cfg,
+                                                               const uint2* __restrict__ lookup,
+                                                               const f4* __restrict__ st, SphSlots sl,
+                                                               uint32_t nparts, uint32_t n) {
+  const uint32_t m = *a.n_out;
+  const uint32_t per = (nparts + 1023u) / 1024u, b0 = threadIdx.x * per;
+  uint32_t sum = 0;
+  for (uint32_t k = 0; k < per; ++k)
+    if (b0 + k < nparts) sum += a.part[b0 + k];
+  uint32_t total;
+  uint32_t pre = block_exclusive_scan<1024>(sum, &total);
+  for (uint32_t k = 0; k < per; ++k)
+    if (b0 + k < nparts) {
+      const uint32_t v = a.part[b0 + k];
+      a.part[b0 + k] = pre;
+      pre += v;
+    }
+  // The listed runs (first particle outside the grid, or longer than kRunScan), after the
+  // grid's, in list order.
+  uint32_t base = total;
+  for (uint32_t c = 0; c < m; c += 1024u) {
+    const uint32_t j = c + threadIdx.x;
+    uint32_t key = 0, t = 0, len = 0;
+    if (j < m) {
+      t = a.out_keys[j];
+      key = lookup[t].x;
+      len = 1;
+      while (t + len < n && lookup[t + len].x == key) ++len;
+    }
+    uint32_t tot;
+    const uint32_t p = base + block_exclusive_scan<1024>(len, &tot);
+    if (j < m) {
+      a.run2[key] = make_uint2(p, p + len);
+      for (uint32_t r = 0; r < len; ++r) predict_slot(cfg, st, sl, p + r, lookup[t + r].y);
+    }
+    base += tot;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) *a.n_out = 0u;  // for the next frame's runs kernel
+}
+
+// Storage runs of a block of 256 cells, and pass 4's prediction (predict_slot) for the
+// block's storage range [bases, bases + its run lengths) in storage order: lane k takes
+// storage slots k, k + 256, ... and finds the cell owning each by a binary search over the
+// block's run bases in LDS, so every lane has the same work whatever the run lengths.
+__global__ __launch_bounds__(kBlock) void sph_layout_write_kernel(SphLayoutArgs a,
+                                                                  const rps_config* __restrict__ cfg,
+                                                                  const uint2* __restrict__ lookup,
+                                                                  const f4* __restrict__ st, SphSlots sl,
+                                                                  uint32_t N) {
+  __shared__ uint32_t lbase[kBlock], lsrc[kBlock];
+  const uint32_t e = blockIdx.x * kBlock + threadIdx.x;
+  const uint2 info = e < a.g.cells ? a.cell_info[e] : make_uint2(0u, 0u);
+  const uint32_t b0 = a.part[blockIdx.x];
+  uint32_t tot;
+  const uint32_t rel = block_exclusive_scan<kBlock>(info.y, &tot);
+  lbase[threadIdx.x] = rel;
+  lsrc[threadIdx.x] = info.x;
+  if (e < a.g.cells) {
+    if (info.y) {
+      a.cell_info[e] = make_uint2(0u, 0u);  // empty again for the next frame's runs kernel
+      int32_t cx, cy;
+      grid_cell(a.g, e, cx, cy);  // the owner's key is its cell's key (sph_runs_kernel)
+      const uint2 run = make_uint2(b0 + rel, b0 + rel + info.y);
+      a.run2[cell_key(cx, cy, N)] = run;
+      a.cellrun[e] = run;
+    } else {
+      a.cellrun[e] = make_uint2(kCellPending, 0u);
+    }
+  }
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < tot; k += kBlock) {
+    uint32_t lo = 0;  // the last cell whose base is <= k (it owns storage slot k)
+#pragma unroll
+    for (uint32_t step = kBlock / 2; step; step >>= 1)
+      if (lbase[lo + step] <= k) lo += step;
+    predict_slot(cfg, st, sl, b0 + k, lookup[lsrc[lo] + (k - lbase[lo])].y);
+  }
+}
+
+// Cells owning no run take their key's storage run from run2 (complete after the write pass).
+__global__ __launch_bounds__(kBlock) void sph_layout_fixup_kernel(SphLayoutArgs a, uint32_t N) {
+  const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+  if (c >= a.g.cells) return;
+  if (a.cellrun[c].x == kCellPending) {
+    int32_t cx, cy;
+    grid_cell(a.g, c, cx, cy);
+    a.cellrun[c] = a.run2[cell_key(cx, cy, N)];
   }
 }
 
@@ -1556,8 +1799,8 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
     const int k = v && *v ? std::atoi(v) : 0;  // 0: by tile size (below)
     return k < 0 ? 0 : (k > 4 ? 4 : k);
   }();
-  const SortBin bin{b.cfg, b.st, b.offsets, b.n};
-  const SortBin nobin{nullptr, nullptr, nullptr, 0u};
+  const SortBin bin{b.cfg, b.st, b.offsets, b.n, b.lay.run2};
+  const SortBin nobin{nullptr, nullptr, nullptr, 0u, nullptr};
   if (stages == 0) {  // P == 1: nothing to sort, only bin
     hipLaunchKernelGGL((sph_sort_local_kernel<true, 1>), dim3(1), dim3(64), 0, s, b.lookup, 1u, 1u, 0u,
                        0u, bin, 0u);
@@ -1704,15 +1947,31 @@ static uint32_t sph_lds_extra(const char* name) {
   return (uint32_t)(k < 0 ? 0 : (k > 65536 ? 65536 : k));
 }
 
-hipError_t launch_sph_pre(const SphBuffers& b, hipStream_t s, bool with_offsets) {
+// XCD-banded workgroups for the slot-order passes (RPS_SPH_XCD=1: with the spatial layout,
+// where a band of slots is a band of space; 2: always; default off: measured slower).
+static uint32_t sph_xcd(const SphBuffers& b) {
+  static const int env = [] {
+    const char* v = std::getenv("RPS_SPH_XCD");
+    return v && *v ? std::atoi(v) : 0;
+  }();
+  return env == 2 ? 1u : (env == 1 ? (uint32_t)b.layout : 0u);
+}
+
+static RunBounds run_bounds(const SphBuffers& b) {
+  return RunBounds{b.offsets, b.ends, b.lay.cellrun, b.lay.run2, b.lay.g};
+}
+
+static hipError_t launch_sph_density(const SphBuffers& b, hipStream_t s) {
   static const uint32_t lds_d = sph_lds_extra("RPS_SPH_DENSITY_LDS");
-  hipLaunchKernelGGL(sph_predict_kernel, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg, b.lookup,
-                     b.st, b.sl, b.p, b.offsets, b.ends, with_offsets ? b.n : 0u);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-#define RPS_DENSITY(B)                                                                           \
-  hipLaunchKernelGGL(sph_density_kernel<B>, dim3(blocks_for(b.p)), dim3(kBlock), lds_d, s, b.cfg, \
-                     b.offsets, b.ends, b.sl, b.p)
+  const uint32_t xcd = sph_xcd(b);
+  const RunBounds rb = run_bounds(b);
+#define RPS_DENSITY(B)                                                                            \
+  if (b.layout)                                                                                   \
+    hipLaunchKernelGGL((sph_density_kernel<B, true>), dim3(blocks_for(b.p)), dim3(kBlock), lds_d, s, \
+                       b.cfg, rb, b.sl, b.p, xcd);                                               \
+  else                                                                                            \
+    hipLaunchKernelGGL((sph_density_kernel<B, false>), dim3(blocks_for(b.p)), dim3(kBlock), lds_d, s, \
+                       b.cfg, rb, b.sl, b.p, xcd)
   switch (sph_batch(true, b.p, b.batch_d)) {
     case 4: RPS_DENSITY(4); break;
     case 16: RPS_DENSITY(16); break;
@@ -1722,15 +1981,68 @@ hipError_t launch_sph_pre(const SphBuffers& b, hipStream_t s, bool with_offsets)
   return hipGetLastError();
 }
 
+hipError_t launch_sph_pre(const SphBuffers& b, hipStream_t s, bool with_offsets) {
+  hipLaunchKernelGGL(sph_predict_kernel, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg, b.lookup, b.st,
+                     b.sl, b.p, b.offsets, b.ends, with_offsets ? b.n : 0u);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return launch_sph_density(b, s);
+}
+
+bool sph_layout_grid(const rps_config& c, uint32_t cell_cap, SphGrid* g) {
+  if (cell_cap == 0) return false;
+  const float r = c.smoothing_radius;
+  // The cells of positions inside the walls, as the bin pass computes them (+1 cell margin).
+  const double x0 = std::floor(((double)c.screen_bounds[0] + c.screen_bounds[1]) / r) - 1.0;
+  const double x1 = std::floor(((double)c.screen_bounds[1] + c.screen_bounds[1]) / r) + 1.0;
+  const double y0 = std::floor(((double)c.screen_bounds[2] + c.screen_bounds[3]) / r) - 1.0;
+  const double y1 = std::floor(((double)c.screen_bounds[3] + c.screen_bounds[3]) / r) + 1.0;
+  if (!(x1 >= x0) || !(y1 >= y0) || x0 < -2.0e9 || y0 < -2.0e9 || x1 > 2.0e9 || y1 > 2.0e9) return false;
+  const double w = x1 - x0 + 1.0, h = y1 - y0 + 1.0;
+  const double tw = std::ceil(w / 8.0), th = std::ceil(h / 8.0);
+  if (tw * th * 64.0 > (double)cell_cap) return false;
+  g->cx_lo = (int32_t)x0;
+  g->cy_lo = (int32_t)y0;
+  g->w = (uint32_t)w;
+  g->h = (uint32_t)h;
+  g->tw = (uint32_t)tw;
+  g->cells = (uint32_t)(tw * th * 64.0);
+  return true;
+}
+
+hipError_t launch_sph_layout_pre(const SphBuffers& b, hipStream_t s) {
+  const SphLayoutArgs& a = b.lay;
+  hipLaunchKernelGGL(sph_runs_kernel, dim3(blocks_for(b.n)), dim3(kBlock), 0, s, a, b.cfg, b.lookup, b.st, b.n);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const uint32_t nparts = blocks_for(a.g.cells);
+  hipLaunchKernelGGL(sph_layout_count_kernel, dim3(nparts), dim3(kBlock), 0, s, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(sph_layout_scan_kernel, dim3(1), dim3(1024), 0, s, a, b.cfg, b.lookup, b.st, b.sl,
+                     nparts, b.n);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(sph_layout_write_kernel, dim3(nparts), dim3(kBlock), 0, s, a, b.cfg, b.lookup, b.st,
+                     b.sl, b.n);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(sph_layout_fixup_kernel, dim3(nparts), dim3(kBlock), 0, s, a, b.n);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  return launch_sph_density(b, s);
+}
+
 hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s) {
   static const uint32_t lds_s = sph_lds_extra("RPS_SPH_SIM_LDS");
-#define RPS_SIM(B)                                                                              \
-  if (b.p == b.n)                                                                              \
-    hipLaunchKernelGGL((sph_sim_kernel<B, false>), dim3(blocks_for(b.p)), dim3(kBlock), lds_s, s, \
-                       b.cfg, b.offsets, b.ends, b.sl, b.st, b.p);                            \
-  else                                                                                         \
-    hipLaunchKernelGGL((sph_sim_kernel<B, true>), dim3(blocks_for(b.p)), dim3(kBlock), lds_s, s, \
-                       b.cfg, b.offsets, b.ends, b.sl, b.st, b.p)
+  const RunBounds rb = run_bounds(b);
+  const uint32_t xcd = sph_xcd(b);
+#define RPS_SIM(B)                                                                                  \
+  if (b.layout)                                                                                     \
+    hipLaunchKernelGGL((sph_sim_kernel<B, false, true>), dim3(blocks_for(b.p)), dim3(kBlock), lds_s, s, \
+                       b.cfg, rb, b.sl, b.st, b.p, xcd);                                           \
+  else if (b.p == b.n)                                                                              \
+    hipLaunchKernelGGL((sph_sim_kernel<B, false, false>), dim3(blocks_for(b.p)), dim3(kBlock), lds_s, s, \
+                       b.cfg, rb, b.sl, b.st, b.p, xcd);                                           \
+  else                                                                                              \
+    hipLaunchKernelGGL((sph_sim_kernel<B, true, false>), dim3(blocks_for(b.p)), dim3(kBlock), lds_s, s, \
+                       b.cfg, rb, b.sl, b.st, b.p, xcd)
   switch (sph_batch(false, b.p, b.batch_s)) {
     case 4: RPS_SIM(4); break;
     case 6: RPS_SIM(6); break;
@@ -1744,8 +2056,8 @@ hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s) {
 uint32_t sph_count_blocks(uint32_t p_slots) { return blocks_for(p_slots); }
 
 hipError_t launch_sph_count(const SphBuffers& b, unsigned long long* out, hipStream_t s) {
-  hipLaunchKernelGGL(sph_count_kernel, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg, b.offsets, b.ends,
-                     b.sl.pp_s, b.p, out);
+  hipLaunchKernelGGL(sph_count_kernel, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg,
+                     b.offsets, b.ends, b.layout ? b.lay.run2 : nullptr, b.sl.pp_s, b.p, out);
   return hipGetLastError();
 }
 

@@ -233,3 +233,60 @@ def test_sph_frame_cost_counts(gpu, orc, n):
     assert cost["sim_bytes"] == 32.0 * scanned + 156.0 * P
     assert unit == "bytes" and amt == cost["frame_bytes"]
     assert cost["frame_bytes"] == cost["sort_bytes"] + cost["predict_bytes"] + cost["density_bytes"] + cost["sim_bytes"]
+
+
+@pytest.mark.parametrize("case", ["blob", "dense", "outside", "xcd"])
+def test_sph_spatial_layout_forced(gpu, orc, monkeypatch, case):
+    """The spatial record layout (rps_kernels.hip; by default only from 2^21 particles) forced
+    at small P == N, every pass bitwise: an ordinary blob; a dense one whose runs exceed the
+    runs kernel's 32-entry measure (the listed-run path); particles far outside the walls
+    (runs owned by cells beyond the grid, lanes whose 3 x 3 block leaves it) with a radius +
+    bounds change mid-run (a new grid); XCD-banded workgroups."""
+    rps = gpu
+    monkeypatch.setenv("RPS_SPH_LAYOUT", "2")
+    n = 16384
+    cfg = rps.default_particle_config(n, gravity=100.0)
+    cfg_at = None
+    if case == "dense":
+        soa = _blob(n, 21, spread=12.0)
+    else:
+        soa = _blob(n, 22, spread=300.0)
+    if case == "outside":
+        soa["x"][:50] = np.float32(2000.0)
+        soa["y"][50:100] = np.float32(-3000.0)
+        soa["x"][100:140] = np.float32(961.0)
+        cfg_at = {2: rps.default_particle_config(n, gravity=100.0, smoothing_radius=14.0,
+                                                 screen_bounds=rps.screen_bounds_for(2400.0, 1400.0))}
+    if case == "xcd":
+        monkeypatch.setenv("RPS_SPH_XCD", "1")
+    _frames_vs_oracle(rps, orc, n, soa, cfg, 4, cfg_at=cfg_at)
+
+
+def test_sph_spatial_layout_gated_frames(gpu, orc, monkeypatch):
+    """Layout frames after gated ones (SHADER_DELAY 5) and a config change that resets
+    frame_count (gated again), at P == N with the layout forced: lookup, offsets, state."""
+    rps = gpu
+    monkeypatch.setenv("RPS_SPH_LAYOUT", "2")
+    n = 8192
+    cfg = rps.default_particle_config(n, gravity=100.0)
+    soa = _blob(n, 31)
+    ext = rps.make_ext()
+    st = orc.SphState(n)
+    ref = copy_soa(soa)
+    with rps.Context(n, rps.MODE_SPH) as ctx:
+        ctx.set_config(cfg, ext)
+        ctx.upload_soa(soa)
+        fc = 0
+        for frame in range(14):
+            if frame == 8:
+                cfg = rps.default_particle_config(n, gravity=50.0)
+                ctx.set_config(cfg, ext)
+                fc = 0
+            ctx.step(1)
+            fc += 1
+            st.grid(cfg, ref)
+            if fc >= 5:
+                st.pre(cfg, ref)
+                st.sim(cfg, ref)
+            assert_bitwise(ctx.read_debug(rps.DEBUG_LOOKUP_OFFSETS), st.offsets, f"offsets f{frame}")
+            assert_soa_bitwise(ctx.download_soa(), ref, what=f"f{frame} ")
