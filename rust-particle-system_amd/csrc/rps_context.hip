@@ -585,10 +585,11 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     // 0.609; 2^20 0.385 -> 0.391 and 2^18 0.166 -> 0.176 slower: DESIGN.md §5), 2 at any P == N.
     const int lay_mode = env_int("RPS_SPH_LAYOUT", 1);
     if (P == n && (lay_mode == 2 || (lay_mode == 1 && n >= (1u << 21)))) {
-      // Up to 2 cells per particle (the bench's viewport has ~0.5).
-      ctx->cell_cap = (uint32_t)std::max<size_t>(2 * n, 4096);
+      // Up to 1 cell per particle (the bench's viewport, like the reference default, has
+      // ~0.52), and at least the reference's default 1920 x 1080 viewport (~27 000 cells).
+      ctx->cell_cap = (uint32_t)std::max<size_t>(n, 1u << 16);
       const size_t cap = ctx->cell_cap;
-      slots.push_back({(void**)&ctx->lay.cell_info, align_up(cap * sizeof(uint2), 256)});
+      slots.push_back({(void**)&ctx->lay.cell_info, align_up(cap * 2 * sizeof(uint4), 256)});
       slots.push_back({(void**)&ctx->lay.cellrun, align_up(cap * sizeof(uint2), 256)});
       slots.push_back({(void**)&ctx->lay.run2, align_up(n * sizeof(uint2), 256)});
       slots.push_back({(void**)&ctx->lay.part, align_up((cap / 256 + 1) * sizeof(uint32_t), 256)});

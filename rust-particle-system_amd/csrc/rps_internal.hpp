@@ -112,7 +112,8 @@ struct SphGrid {
 };
 struct SphLayoutArgs {
   SphGrid g;
-  uint2* cell_info;    // cells: {first slot, length} of the run a cell owns ({0, 0}: none)
+  uint4* cell_info;    // 2 x cells: {first slot, length, 6 particle indices} of the run a cell
+                       //   owns (length 0: none)
   uint2* cellrun;      // cells: storage {start, end} of the cell's key's run (start >= N: none)
   uint2* run2;         // N: storage {start, end} per key ({0xFFFFFFFF, 0}: none; reset in bin)
   uint32_t* part;      // cells / 256 + 1: 256-cell block sums -> bases (0 between frames)
@@ -142,7 +143,7 @@ bool sph_layout_grid(const rps_config& c, uint32_t cell_cap, SphGrid* g);
 // fixup, density.
 hipError_t launch_sph_layout_pre(const SphBuffers& b, hipStream_t s);
 // Scan batch of the density (`density`) or sim pass at P entries; `forced` != 0 wins.
-int sph_batch(bool density, uint32_t p, int forced);
+int sph_batch(bool density, uint32_t p, int forced, bool layout);
 // Runs the whole bitonic network of src/particle_compute.rs:117-149; returns the number of
 // reference passes covered (S(S+1)/2) in *passes.
 hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,

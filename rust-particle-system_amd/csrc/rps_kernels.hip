@@ -935,6 +935,7 @@ __global__ __launch_bounds__(kBlock) void sph_offsets_kernel(const uint2* __rest
 constexpr uint32_t kCellOut = 0xFFFFFFFFu;
 constexpr uint32_t kCellPending = 0xFFFFFFFEu;  // cellrun entry to resolve through run2
 constexpr uint32_t kRunScan = 32u;               // longest run a runs-kernel lane measures itself
+constexpr uint32_t kRunIdx = 6u;                 // particle indices a run's cell_info records
 
 __device__ __forceinline__ uint32_t grid_enum_xy(const SphGrid& g, uint32_t x, uint32_t y) {
   return (((y >> 3) * g.tw + (x >> 3)) << 6) | ((y & 7u) << 3) | (x & 7u);
@@ -1449,22 +1450,40 @@ __global__ __launch_bounds__(kBlock) void sph_runs_kernel(SphLayoutArgs a, const
   // The cell of the run's first particle, computed as the bin pass did (same state, same
   // ops), so its key is e.x; anything else (never seen) is handled as outside the grid.
   const f4 s = st[e.y];
+  // Length, and the first kRunIdx particle indices (the write pass then needs no lookup
+  // gathers for them).
+  uint32_t idx[kRunIdx];
+  idx[0] = e.y;
   uint32_t len = 1;
-  while (len <= kRunScan && t + len < n && lookup[t + len].x == e.x) ++len;
+#pragma unroll
+  for (uint32_t k = 1; k < kRunIdx; ++k) {
+    idx[k] = 0u;
+    if (len == k && t + k < n) {
+      const uint2 v = lookup[t + k];
+      if (v.x == e.x) {
+        idx[k] = v.y;
+        len = k + 1u;
+      }
+    }
+  }
+  if (len == kRunIdx)
+    while (len <= kRunScan && t + len < n && lookup[t + len].x == e.x) ++len;
   const float r = cfg->smoothing_radius;
   const int32_t cx = f32_to_i32((s[0] + cfg->screen_bounds[1]) / r);
   const int32_t cy = f32_to_i32((s[1] + cfg->screen_bounds[3]) / r);
   const uint32_t c = cell_key(cx, cy, cfg->particle_count) == e.x ? grid_enum(a.g, cx, cy) : kCellOut;
-  if (c == kCellOut || len > kRunScan)
+  if (c == kCellOut || len > kRunScan) {
     a.out_keys[atomicAdd(a.n_out, 1u)] = t;  // placed by the scan kernel
-  else
-    a.cell_info[c] = make_uint2(t, len);
+  } else {
+    a.cell_info[2u * c] = make_uint4(t, len, idx[0], idx[1]);
+    a.cell_info[2u * c + 1u] = make_uint4(idx[2], idx[3], idx[4], idx[5]);
+  }
 }
 
 // Run lengths owned by each 256-cell block.
 __global__ __launch_bounds__(kBlock) void sph_layout_count_kernel(SphLayoutArgs a) {
   const uint32_t e = blockIdx.x * kBlock + threadIdx.x;
-  const uint32_t len = e < a.g.cells ? a.cell_info[e].y : 0u;
+  const uint32_t len = e < a.g.cells ? a.cell_info[2u * e].y : 0u;
   uint32_t tot;
   block_exclusive_scan<kBlock>(len, &tot);
   if (threadIdx.x == 0) a.part[blockIdx.x] = tot;
@@ -1514,27 +1533,41 @@ __global__ __launch_bounds__(1024) void sph_layout_scan_kernel(SphLayoutArgs a,
 
 // Storage runs of a block of 256 cells, and pass 4's prediction (predict_slot) for the
 // block's storage range [bases, bases + its run lengths) in storage order: lane k takes
-// storage slots k, k + 256, ... and finds the cell owning each by a binary search over the
-// block's run bases in LDS, so every lane has the same work whatever the run lengths.
+// storage slots k, k + 256, ..., so every lane has the same work whatever the run lengths.
+// The cell owning slot k comes from an LDS map the owners fill (slots < kSlotMap; beyond it,
+// a binary search over the block's run bases), its particle index from the indices the runs
+// kernel recorded (run entries < kRunIdx; beyond them, the lookup).
+constexpr uint32_t kSlotMap = 2048;
 __global__ __launch_bounds__(kBlock) void sph_layout_write_kernel(SphLayoutArgs a,
                                                                   const rps_config* __restrict__ cfg,
                                                                   const uint2* __restrict__ lookup,
                                                                   const f4* __restrict__ st, SphSlots sl,
                                                                   uint32_t N) {
-  __shared__ uint32_t lbase[kBlock], lsrc[kBlock];
+  __shared__ uint32_t lbase[kBlock], lsrc[kBlock], lidx[kRunIdx][kBlock];
+  __shared__ uint8_t lcell[kSlotMap];
   const uint32_t e = blockIdx.x * kBlock + threadIdx.x;
-  const uint2 info = e < a.g.cells ? a.cell_info[e] : make_uint2(0u, 0u);
+  const bool in = e < a.g.cells;
+  const uint4 i0 = in ? a.cell_info[2u * e] : make_uint4(0u, 0u, 0u, 0u);
+  const uint4 i1 = in ? a.cell_info[2u * e + 1u] : make_uint4(0u, 0u, 0u, 0u);
+  const uint32_t len = i0.y;
   const uint32_t b0 = a.part[blockIdx.x];
   uint32_t tot;
-  const uint32_t rel = block_exclusive_scan<kBlock>(info.y, &tot);
+  const uint32_t rel = block_exclusive_scan<kBlock>(len, &tot);
   lbase[threadIdx.x] = rel;
-  lsrc[threadIdx.x] = info.x;
-  if (e < a.g.cells) {
-    if (info.y) {
-      a.cell_info[e] = make_uint2(0u, 0u);  // empty again for the next frame's runs kernel
+  lsrc[threadIdx.x] = i0.x;
+  lidx[0][threadIdx.x] = i0.z;
+  lidx[1][threadIdx.x] = i0.w;
+  lidx[2][threadIdx.x] = i1.x;
+  lidx[3][threadIdx.x] = i1.y;
+  lidx[4][threadIdx.x] = i1.z;
+  lidx[5][threadIdx.x] = i1.w;
+  for (uint32_t r = 0; r < len && rel + r < kSlotMap; ++r) lcell[rel + r] = (uint8_t)threadIdx.x;
+  if (in) {
+    if (len) {
+      a.cell_info[2u * e] = make_uint4(0u, 0u, 0u, 0u);  // empty again for the next frame
       int32_t cx, cy;
       grid_cell(a.g, e, cx, cy);  // the owner's key is its cell's key (sph_runs_kernel)
-      const uint2 run = make_uint2(b0 + rel, b0 + rel + info.y);
+      const uint2 run = make_uint2(b0 + rel, b0 + rel + len);
       a.run2[cell_key(cx, cy, N)] = run;
       a.cellrun[e] = run;
     } else {
@@ -1543,11 +1576,18 @@ __global__ __launch_bounds__(kBlock) void sph_layout_write_kernel(SphLayoutArgs 
   }
   __syncthreads();
   for (uint32_t k = threadIdx.x; k < tot; k += kBlock) {
-    uint32_t lo = 0;  // the last cell whose base is <= k (it owns storage slot k)
+    uint32_t lo;
+    if (k < kSlotMap) {
+      lo = lcell[k];
+    } else {  // the last cell whose base is <= k
+      lo = 0;
 #pragma unroll
-    for (uint32_t step = kBlock / 2; step; step >>= 1)
-      if (lbase[lo + step] <= k) lo += step;
-    predict_slot(cfg, st, sl, b0 + k, lookup[lsrc[lo] + (k - lbase[lo])].y);
+      for (uint32_t step = kBlock / 2; step; step >>= 1)
+        if (lbase[lo + step] <= k) lo += step;
+    }
+    const uint32_t r = k - lbase[lo];
+    const uint32_t i = r < kRunIdx ? lidx[r][lo] : lookup[lsrc[lo] + r].y;
+    predict_slot(cfg, st, sl, b0 + k, i);
   }
 }
 
@@ -1922,8 +1962,11 @@ hipError_t launch_sph_offsets(const SphBuffers& b, hipStream_t s) {
 // Entries in flight per lane in the density and sim scans, unless the context forces one
 // (SphBuffers::batch_d / batch_s, from RPS_SPH_BATCH[_D|_S] at rps_create): by size, measured
 // (DESIGN.md §5).
-int sph_batch(bool density, uint32_t p, int forced) {
+int sph_batch(bool density, uint32_t p, int forced, bool layout) {
   if (forced == 4 || forced == 6 || forced == 8 || forced == 16) return forced;
+  // With the spatial record layout the sim's gathers hit the caches: 4 at 2^22 too (1.1251 ->
+  // 1.1018 ms/frame; 8: 1.1607), as below 2^21.
+  if (!density && layout) return 4;
   // The sim scan keeps 4 entries in flight up to P = 2^21, where its slot records stay in
   // the caches (2^20 frame 0.404 -> 0.392 ms, 2^21 0.670 -> 0.651), and 6 beyond (2^22: 1.2223
   // ms with 8, 1.2129 with 6 -- 91 VGPRs, 5 waves/SIMD instead of 111 and 4 --, 1.28 with 4,
@@ -1972,7 +2015,7 @@ static hipError_t launch_sph_density(const SphBuffers& b, hipStream_t s) {
   else                                                                                            \
     hipLaunchKernelGGL((sph_density_kernel<B, false>), dim3(blocks_for(b.p)), dim3(kBlock), lds_d, s, \
                        b.cfg, rb, b.sl, b.p, xcd)
-  switch (sph_batch(true, b.p, b.batch_d)) {
+  switch (sph_batch(true, b.p, b.batch_d, b.layout)) {
     case 4: RPS_DENSITY(4); break;
     case 16: RPS_DENSITY(16); break;
     default: RPS_DENSITY(8); break;
@@ -2043,7 +2086,7 @@ hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s) {
   else                                                                                              \
     hipLaunchKernelGGL((sph_sim_kernel<B, true, false>), dim3(blocks_for(b.p)), dim3(kBlock), lds_s, s, \
                        b.cfg, rb, b.sl, b.st, b.p, xcd)
-  switch (sph_batch(false, b.p, b.batch_s)) {
+  switch (sph_batch(false, b.p, b.batch_s, b.layout)) {
     case 4: RPS_SIM(4); break;
     case 6: RPS_SIM(6); break;
     case 16: RPS_SIM(16); break;

@@ -235,13 +235,15 @@ def test_sph_frame_cost_counts(gpu, orc, n):
     assert cost["frame_bytes"] == cost["sort_bytes"] + cost["predict_bytes"] + cost["density_bytes"] + cost["sim_bytes"]
 
 
-@pytest.mark.parametrize("case", ["blob", "dense", "outside", "xcd"])
+@pytest.mark.parametrize("case", ["blob", "dense", "outside", "xcd", "batches"])
 def test_sph_spatial_layout_forced(gpu, orc, monkeypatch, case):
     """The spatial record layout (rps_kernels.hip; by default only from 2^21 particles) forced
     at small P == N, every pass bitwise: an ordinary blob; a dense one whose runs exceed the
     runs kernel's 32-entry measure (the listed-run path); particles far outside the walls
     (runs owned by cells beyond the grid, lanes whose 3 x 3 block leaves it) with a radius +
-    bounds change mid-run (a new grid); XCD-banded workgroups."""
+    bounds change mid-run (a new grid); XCD-banded workgroups; other scan batches.  The
+    16 384-particle default viewport has ~28 700 cells, within the context's cell capacity
+    (at least 2^16), so every frame here runs the layout."""
     rps = gpu
     monkeypatch.setenv("RPS_SPH_LAYOUT", "2")
     n = 16384
@@ -259,6 +261,9 @@ def test_sph_spatial_layout_forced(gpu, orc, monkeypatch, case):
                                                  screen_bounds=rps.screen_bounds_for(2400.0, 1400.0))}
     if case == "xcd":
         monkeypatch.setenv("RPS_SPH_XCD", "1")
+    if case == "batches":  # the layout's other scan variants (default: density 8, sim 4)
+        monkeypatch.setenv("RPS_SPH_BATCH_S", "6")
+        monkeypatch.setenv("RPS_SPH_BATCH_D", "16")
     _frames_vs_oracle(rps, orc, n, soa, cfg, 4, cfg_at=cfg_at)
 
 
