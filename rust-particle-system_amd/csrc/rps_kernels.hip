@@ -937,8 +937,12 @@ constexpr uint32_t kCellPending = 0xFFFFFFFEu;  // cellrun entry to resolve thro
 constexpr uint32_t kRunScan = 32u;               // longest run a runs-kernel lane measures itself
 constexpr uint32_t kRunIdx = 6u;                 // particle indices a run's cell_info records
 
+#ifndef RPS_CELL_TILE_LOG
+#define RPS_CELL_TILE_LOG 3  // 8 x 8 cells per tile (4 x 4: equal, 16 x 16: slower)
+#endif
+constexpr uint32_t kCT = RPS_CELL_TILE_LOG, kCTM = (1u << kCT) - 1u;
 __device__ __forceinline__ uint32_t grid_enum_xy(const SphGrid& g, uint32_t x, uint32_t y) {
-  return (((y >> 3) * g.tw + (x >> 3)) << 6) | ((y & 7u) << 3) | (x & 7u);
+  return (((y >> kCT) * g.tw + (x >> kCT)) << (2u * kCT)) | ((y & kCTM) << kCT) | (x & kCTM);
 }
 __device__ __forceinline__ uint32_t grid_enum(const SphGrid& g, int32_t cx, int32_t cy) {
   const uint32_t x = (uint32_t)cx - (uint32_t)g.cx_lo, y = (uint32_t)cy - (uint32_t)g.cy_lo;
@@ -948,9 +952,9 @@ __device__ __forceinline__ uint32_t grid_enum(const SphGrid& g, int32_t cx, int3
 
 // Inverse of grid_enum; false for the padding cells of edge tiles.
 __device__ __forceinline__ bool grid_cell(const SphGrid& g, uint32_t e, int32_t& cx, int32_t& cy) {
-  const uint32_t tile = e >> 6;
+  const uint32_t tile = e >> (2u * kCT);
   const uint32_t ty = tile / g.tw;
-  const uint32_t x = (tile - ty * g.tw) * 8u + (e & 7u), y = ty * 8u + ((e >> 3) & 7u);
+  const uint32_t x = ((tile - ty * g.tw) << kCT) + (e & kCTM), y = (ty << kCT) + ((e >> kCT) & kCTM);
   cx = (int32_t)((uint32_t)g.cx_lo + x);
   cy = (int32_t)((uint32_t)g.cy_lo + y);
   return x < g.w && y < g.h;
@@ -2042,14 +2046,15 @@ bool sph_layout_grid(const rps_config& c, uint32_t cell_cap, SphGrid* g) {
   const double y1 = std::floor(((double)c.screen_bounds[3] + c.screen_bounds[3]) / r) + 1.0;
   if (!(x1 >= x0) || !(y1 >= y0) || x0 < -2.0e9 || y0 < -2.0e9 || x1 > 2.0e9 || y1 > 2.0e9) return false;
   const double w = x1 - x0 + 1.0, h = y1 - y0 + 1.0;
-  const double tw = std::ceil(w / 8.0), th = std::ceil(h / 8.0);
-  if (tw * th * 64.0 > (double)cell_cap) return false;
+  const double ts = (double)(1u << kCT);
+  const double tw = std::ceil(w / ts), th = std::ceil(h / ts);
+  if (tw * th * ts * ts > (double)cell_cap) return false;
   g->cx_lo = (int32_t)x0;
   g->cy_lo = (int32_t)y0;
   g->w = (uint32_t)w;
   g->h = (uint32_t)h;
   g->tw = (uint32_t)tw;
-  g->cells = (uint32_t)(tw * th * 64.0);
+  g->cells = (uint32_t)(tw * th * ts * ts);
   return true;
 }
 
