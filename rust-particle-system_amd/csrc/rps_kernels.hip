@@ -941,8 +941,23 @@ constexpr uint32_t kRunIdx = 6u;                 // particle indices a run's cel
 #define RPS_CELL_TILE_LOG 3  // 8 x 8 cells per tile (4 x 4: equal, 16 x 16: slower)
 #endif
 constexpr uint32_t kCT = RPS_CELL_TILE_LOG, kCTM = (1u << kCT) - 1u;
+#ifndef RPS_TILE_COLMAJOR
+#define RPS_TILE_COLMAJOR 0  // tiles column by column (slower, below)
+#endif
+#ifndef RPS_CELL_COLMAJOR
+// Cells within a tile column by column: the scans walk a particle's nine runs column by column
+// (GRID_OFFSETS, wgsl:200-204), so each column's three runs are adjacent in storage (2^22
+// 1.1003 -> 1.0873 ms/frame; tiles column by column too: 1.0968; 16 x 16: 1.0917, 4 x 4: 1.0961).
+#define RPS_CELL_COLMAJOR 1
+#endif
 __device__ __forceinline__ uint32_t grid_enum_xy(const SphGrid& g, uint32_t x, uint32_t y) {
-  return (((y >> kCT) * g.tw + (x >> kCT)) << (2u * kCT)) | ((y & kCTM) << kCT) | (x & kCTM);
+  const uint32_t in_tile = RPS_CELL_COLMAJOR ? (((x & kCTM) << kCT) | (y & kCTM)) : (((y & kCTM) << kCT) | (x & kCTM));
+#if RPS_TILE_COLMAJOR
+  const uint32_t th = (g.cells >> (2u * kCT)) / g.tw;
+  return (((x >> kCT) * th + (y >> kCT)) << (2u * kCT)) | in_tile;
+#else
+  return (((y >> kCT) * g.tw + (x >> kCT)) << (2u * kCT)) | in_tile;
+#endif
 }
 __device__ __forceinline__ uint32_t grid_enum(const SphGrid& g, int32_t cx, int32_t cy) {
   const uint32_t x = (uint32_t)cx - (uint32_t)g.cx_lo, y = (uint32_t)cy - (uint32_t)g.cy_lo;
@@ -953,8 +968,16 @@ __device__ __forceinline__ uint32_t grid_enum(const SphGrid& g, int32_t cx, int3
 // Inverse of grid_enum; false for the padding cells of edge tiles.
 __device__ __forceinline__ bool grid_cell(const SphGrid& g, uint32_t e, int32_t& cx, int32_t& cy) {
   const uint32_t tile = e >> (2u * kCT);
-  const uint32_t ty = tile / g.tw;
-  const uint32_t x = ((tile - ty * g.tw) << kCT) + (e & kCTM), y = (ty << kCT) + ((e >> kCT) & kCTM);
+#if RPS_TILE_COLMAJOR
+  const uint32_t th = (g.cells >> (2u * kCT)) / g.tw;
+  const uint32_t tx_ = tile / th, ty = tile - tx_ * th;
+  const uint32_t tile_rm = ty * g.tw + tx_;  // the same tile in row-major numbering
+#else
+  const uint32_t ty = tile / g.tw, tile_rm = tile;
+#endif
+  const uint32_t lo = RPS_CELL_COLMAJOR ? ((e >> kCT) & kCTM) : (e & kCTM);
+  const uint32_t hi = RPS_CELL_COLMAJOR ? (e & kCTM) : ((e >> kCT) & kCTM);
+  const uint32_t x = ((tile_rm - ty * g.tw) << kCT) + lo, y = (ty << kCT) + hi;
   cx = (int32_t)((uint32_t)g.cx_lo + x);
   cy = (int32_t)((uint32_t)g.cy_lo + y);
   return x < g.w && y < g.h;
@@ -1415,7 +1438,8 @@ __global__ __launch_bounds__(kBlock) void sph_count_kernel(const rps_config* __r
 //       and its lookup entries are copied to lookup2 (storage order); cells owning no run
 //       are marked, and the predict pass resolves them through run2 (a key shared by several
 //       cells belongs to one of them).
-// Cells are enumerated in 8 x 8 tiles, tiles row-major over the screen's cell range.
+// Cells are enumerated in 8 x 8 tiles (column by column inside a tile), tiles row-major over
+// the screen's cell range.
 // Exclusive prefix of v over a workgroup of NT threads; *total = the workgroup's sum.
 template <uint32_t NT>
 __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* total) {
@@ -1456,19 +1480,18 @@ __global__ __launch_bounds__(kBlock) void sph_runs_kernel(SphLayoutArgs a, const
   const f4 s = st[e.y];
   // Length, and the first kRunIdx particle indices (the write pass then needs no lookup
   // gathers for them).
+  // The next entries are loaded together (adjacent, mostly one line), then measured.
+  uint2 nx[kRunIdx];
+#pragma unroll
+  for (uint32_t k = 1; k < kRunIdx; ++k) nx[k] = t + k < n ? lookup[t + k] : make_uint2(~e.x, 0u);
   uint32_t idx[kRunIdx];
   idx[0] = e.y;
   uint32_t len = 1;
 #pragma unroll
   for (uint32_t k = 1; k < kRunIdx; ++k) {
-    idx[k] = 0u;
-    if (len == k && t + k < n) {
-      const uint2 v = lookup[t + k];
-      if (v.x == e.x) {
-        idx[k] = v.y;
-        len = k + 1u;
-      }
-    }
+    const bool more = len == k && nx[k].x == e.x;
+    idx[k] = more ? nx[k].y : 0u;
+    len = more ? k + 1u : len;
   }
   if (len == kRunIdx)
     while (len <= kRunScan && t + len < n && lookup[t + len].x == e.x) ++len;
