@@ -1099,15 +1099,26 @@ __device__ __forceinline__ uint32_t nine_runs(const RunBounds& rb, float px, flo
       e[o] = rb.ends[key[o]];
     }
   }
+  // A run that starts where the previous non-empty one ends in memory extends its table
+  // entry (with the spatial layout a column's three runs usually do): fewer run boundaries
+  // for the cursor, the same flat entries.
   uint32_t c = 0, m = 0;
+  uint2 last = make_uint2(0u, 0u);
 #pragma unroll
   for (int o = 0; o < 9; ++o) {
     if (s[o] < N) {
-      runs[m][threadIdx.x] = make_uint2(s[o] - c, c + (e[o] - s[o]));
-      c += e[o] - s[o];
-      ++m;
+      const uint32_t len = e[o] - s[o];
+      if (m && s[o] == last.x + last.y) {
+        last.y += len;
+      } else {
+        if (m) runs[m - 1u][threadIdx.x] = last;
+        last = make_uint2(s[o] - c, c + len);
+        ++m;
+      }
+      c += len;
     }
   }
+  if (m) runs[m - 1u][threadIdx.x] = last;
   return c;
 }
 
