@@ -347,7 +347,11 @@ def sph_side(rps, args, d):
     sim_ms = d.max(sim_ms)
     frame_ms = el * 1e3 / args.sph_frames
     sim_gbps = cost["sim_bytes"] / (sim_ms * 1e-3) / 1e9
+    pow2 = n & (n - 1) == 0
+    layout = os.environ.get("RPS_SPH_LAYOUT", "1")
+    spatial = pow2 and (layout == "2" or (layout == "1" and n >= (1 << 21)))  # rps_context.hip
     out = {"workload": f"SPH frame (5 passes, bitwise == oracle), {n} particles per rank, reference scatter",
+           "record_layout": "cell tiles (spatial)" if spatial else "lookup order",
            "scaling": "replicas", "frames": args.sph_frames, "ms_per_frame": frame_ms,
            "particle_steps_per_s": float(n) * d.world * args.sph_frames / el,
            "sim_kernel_ms": sim_ms,
