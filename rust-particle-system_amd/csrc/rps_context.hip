@@ -52,6 +52,7 @@ struct rps_ctx {
   uint32_t P = 0;
   uint32_t sort_passes = 0, sort_launches = 0;
   uint8_t sph_batch_d = 0, sph_batch_s = 0;  // forced scan batches (0: by size)
+  uint8_t sph_xcd = 0;     // RPS_SPH_XCD at create
   SphLayoutArgs lay{};     // spatial record layout (P == N, RPS_SPH_LAYOUT != 0): arrays
   uint32_t cell_cap = 0;   // their cell capacity (0: no layout)
   bool layout_last = false;  // the last active frame used the layout (slot records in storage order)
@@ -290,6 +291,7 @@ SphBuffers sph_buffers(rps_ctx* ctx) {
   b.p = ctx->P;
   b.batch_d = ctx->sph_batch_d;
   b.batch_s = ctx->sph_batch_s;
+  b.xcd_mode = ctx->sph_xcd;
   b.lay = ctx->lay;
   b.cell_cap = ctx->cell_cap;
   b.layout = ctx->layout_last;
@@ -529,6 +531,8 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     const int both = env_int("RPS_SPH_BATCH", 0);
     ctx->sph_batch_d = (uint8_t)std::max(0, std::min(255, env_int("RPS_SPH_BATCH_D", both)));
     ctx->sph_batch_s = (uint8_t)std::max(0, std::min(255, env_int("RPS_SPH_BATCH_S", both)));
+    // RPS_SPH_XCD (XCD-banded scan workgroups) is per context too, read here like the batches.
+    ctx->sph_xcd = (uint8_t)std::max(0, std::min(2, env_int("RPS_SPH_XCD", 0)));
   }
 
   auto bail = [&](int code) {

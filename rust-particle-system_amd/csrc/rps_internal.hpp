@@ -133,6 +133,7 @@ struct SphBuffers {
   uint32_t p;        // next_pow2(N)
   uint8_t batch_d;   // scan entries in flight per lane, density / sim pass (4, 8, 16;
   uint8_t batch_s;   //   0: by size, sph_batch); per context, RPS_SPH_BATCH[_D|_S] at create
+  uint8_t xcd_mode;  // RPS_SPH_XCD at create: 0 off, 1 with the layout, 2 always
   bool layout;       // this frame uses the spatial record layout (lay.* valid, P == N)
   uint32_t cell_cap; // capacity of lay.cell_info / cellrun (0: layout never available)
   SphLayoutArgs lay;

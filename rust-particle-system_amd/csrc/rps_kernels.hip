@@ -2031,11 +2031,7 @@ static uint32_t sph_lds_extra(const char* name) {
 // XCD-banded workgroups for the slot-order passes (RPS_SPH_XCD=1: with the spatial layout,
 // where a band of slots is a band of space; 2: always; default off: measured slower).
 static uint32_t sph_xcd(const SphBuffers& b) {
-  static const int env = [] {
-    const char* v = std::getenv("RPS_SPH_XCD");
-    return v && *v ? std::atoi(v) : 0;
-  }();
-  return env == 2 ? 1u : (env == 1 ? (uint32_t)b.layout : 0u);
+  return b.xcd_mode == 2 ? 1u : (b.xcd_mode == 1 ? (uint32_t)b.layout : 0u);
 }
 
 static RunBounds run_bounds(const SphBuffers& b) {
