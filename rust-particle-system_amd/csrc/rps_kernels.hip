@@ -1440,17 +1440,19 @@ __global__ __launch_bounds__(kBlock) void sph_count_kernel(const rps_config* __r
 // the same entries in the same order as the reference (bitwise), but the runs of neighbouring
 // cells sit next to each other, and a cell-ordered table of storage runs (cellrun) replaces
 // the scans' key-indexed (hash-random) run bounds:
-//   runs kernel (slot order): offsets/ends as the reference's pass 3; at a run start, the
-//       run's length and the cell of its first particle (its owner): cell_info[cell] =
-//       {first slot, length}, and the length added to the owner's 256-cell block sum;
-//       runs whose first particle lies outside the grid (or longer than kRunScan) go to a list;
-//   scan (one workgroup): block bases; the listed runs placed after the grid's;
-//   write (cell order): each owned run gets the next storage range -> run2[key], cellrun[cell],
-//       and its lookup entries are copied to lookup2 (storage order); cells owning no run
-//       are marked, and the predict pass resolves them through run2 (a key shared by several
+//   runs kernel (slot order, in place of pass 3): at a run start, the run's length and the
+//       cell of its first particle (its owner): cell_info[cell] = {first slot, length, the
+//       first kRunIdx particle indices}; runs whose first particle lies outside the grid (or
+//       longer than kRunScan) go to a list (the reference's offsets are rebuilt on readback);
+//   block counts (256 cells) and one-workgroup scan: block bases; listed runs after the grid's;
+//   write (cell order): each owned run gets the next storage range -> run2[key], cellrun[cell];
+//       then pass 4's prediction for the block's storage range, in storage order; cells
+//       owning no run are marked;
+//   fixup (cell order): marked cells take their key's run from run2 (a key shared by several
 //       cells belongs to one of them).
 // Cells are enumerated in 8 x 8 tiles (column by column inside a tile), tiles row-major over
 // the screen's cell range.
+
 // Exclusive prefix of v over a workgroup of NT threads; *total = the workgroup's sum.
 template <uint32_t NT>
 __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* total) {
