@@ -171,10 +171,10 @@ def test_sph_forced_scan_batches(gpu, orc, monkeypatch, n, batch):
 @pytest.mark.parametrize("n", [1 << 22, 1 << 21])
 def test_sph_bench_workload_full_size(gpu, orc, n):
     """The bench's `sph` workload exactly (2^22): particles of the reference scatter over a
-    viewport scaled to the default density, every frame active.  P > 2^21 selects the sim
-    scan's 6-entry batch, 8192-entry sort tiles with 3 passes per register chunk and the
-    five-pass register-fused global stage; at P = 2^21 (the largest size on the 4-entry sim
-    batch) that stage is a gathered-tile launch.  Two frames, every pass bitwise."""
+    viewport scaled to the default density, every frame active.  Both sizes run the spatial
+    record layout (from 2^21) with its 4-entry sim scan; P = 2^22 selects 8192-entry sort
+    tiles with 3 passes per register chunk and the five-pass register-fused global stage; at
+    P = 2^21 that stage is a gathered-tile launch.  Two frames, every pass bitwise."""
     rps = gpu
     scale = (n / 50000) ** 0.5
     cfg = rps.default_particle_config(n, screen_bounds=rps.screen_bounds_for(1920.0 * scale, 1080.0 * scale))
