@@ -259,6 +259,12 @@ int rps_set_profiling(rps_ctx* ctx, int period);
 /* Average duration (ms) and count of the bracketed dominant-kernel launches since profiling
  * was enabled; blocks until they completed. */
 int rps_get_kernel_time(rps_ctx* ctx, double* avg_ms, uint64_t* launches);
+/* N-body: the shader clock the chip sustained during the most recent profiled force launch
+ * (median over its workgroups of delta s_memtime / delta s_memrealtime x 100 MHz, stamped at
+ * each workgroup's start and end), in MHz, and the number of workgroups it is the median of.
+ * RPS_ERR_UNSUPPORTED before a profiled launch or outside N-body mode.  For reporting FP32
+ * fractions against the clock actually held (MI355X peaks assume 2400 MHz). */
+int rps_get_kernel_clock(rps_ctx* ctx, double* mhz, uint64_t* workgroups);
 /* Time nsteps rps_step calls with a pair of HIP events on the context stream. */
 int rps_time_steps(rps_ctx* ctx, uint32_t nsteps, double* total_ms);
 /* The context's hipStream_t (as void*), for callers that interoperate on the same stream. */
@@ -266,8 +272,10 @@ void* rps_get_stream(rps_ctx* ctx);
 
 /* Algorithmic HBM bytes (stream/SPH) or flops (N-body) one step moves for this context's
  * mode/config; `unit` receives 0 for bytes, 1 for flops.  SPH: the frame's
- * bytes of rps_sph_frame_cost (counts the current state's neighbour entries, blocks). */
-int rps_step_cost(const rps_ctx* ctx, double* amount, int* unit);
+ * bytes of rps_sph_frame_cost, which launches a counting kernel on the context stream and
+ * waits for it (so the context is not const; RPS_ERR_UNSUPPORTED unless the most recent
+ * frame was active).  STREAM / N-body: host arithmetic only. */
+int rps_step_cost(rps_ctx* ctx, double* amount, int* unit);
 
 /* SPH frame cost, for rooflines: the algorithmic bytes of one active frame
  * of the current state.  E = neighbour entries the reference's scans visit (the nine runs of
@@ -278,9 +286,10 @@ int rps_step_cost(const rps_ctx* ctx, double* amount, int* unit);
  *   sim      E x 32 B (pressure {pos, P/rho^2, Pn/(rho rho_n)} + viscosity {pos, v} records)
  *            + P x 156 B (runs, masks, own records, state write)
  * The scans' neighbour records are re-read E/P times per frame and served by the caches, so
- * their roofline is the aggregate L2 bandwidth, not HBM.  Counts the most recent active
- * frame's runs (RPS_ERR_UNSUPPORTED before one): launches a counting kernel on the context
- * stream and waits for it (not for timed regions).  SPH mode only. */
+ * their roofline is the aggregate L2 bandwidth, not HBM.  Counts the most recent frame's
+ * runs, which must have been active (RPS_ERR_UNSUPPORTED otherwise: a gated frame re-sorts
+ * the lookup but keeps older predictions): launches a counting kernel on the context stream
+ * into a buffer allocated at rps_create and waits for it (not for timed regions).  SPH only. */
 typedef struct rps_sph_cost {
   uint64_t slots;            /* P = next_pow2(N) */
   uint64_t particles;        /* N */

@@ -54,6 +54,7 @@ def lib(omp: bool = False) -> ctypes.CDLL:
         "orc_stream_step_omp": (None, [_P, _P, _U64, _U64, _U32, _P, _P, _P, _P, _P, _U64, _I]),
         "orc_init_scatter": (None, [_P, _P, _U64, _U64, _U64, _U32, _P, _P, _P, _P, _P, _U64]),
         "orc_nbody_accel": (None, [_P, _P, _P, _U64, _U64, _U64, _P, _P]),
+        "orc_nbody_accel_ref": (None, [_P, _P, _P, _U64, _U64, _U64, _P, _P, _P]),
         "orc_nbody_accel_f32_omp": (None, [_P, _P, _P, _U64, _U64, _U64, _P, _P, _I]),
         "orc_nbody_integrate": (None, [_P, _P, _P, _P, _P, _P, _P, _P, _U64]),
         "orc_sph_bin": (None, [_P, _P, _P, _P, _P, _U32]),
@@ -210,6 +211,23 @@ def nbody_accel(ext, sx, sy, t0=0, nt=None):
     ay = np.zeros(nt, np.float32)
     lib().orc_nbody_accel(_ref(ext), _p(sx), _p(sy), len(sx), t0, nt, _p(ax), _p(ay))
     return ax, ay
+
+
+def nbody_accel_ref(ext, sx, sy, t0=0, nt=None, threads=0):
+    """orc_nbody_accel's f64 sums for targets [t0, t0 + nt) plus G * sum_j |f_ij| per target
+    (f64), on the OpenMP build (targets over threads; each target's sum in source order, so
+    the same bits as one thread).  Returns (ax, ay, abs_sum)."""
+    sx = np.ascontiguousarray(sx, np.float32)
+    sy = np.ascontiguousarray(sy, np.float32)
+    nt = len(sx) - t0 if nt is None else nt
+    ax = np.zeros(nt, np.float32)
+    ay = np.zeros(nt, np.float32)
+    ab = np.zeros(nt, np.float64)
+    L = lib(omp=True)
+    if threads:
+        L.orc_set_threads(threads)
+    L.orc_nbody_accel_ref(_ref(ext), _p(sx), _p(sy), len(sx), t0, nt, _p(ax), _p(ay), _p(ab))
+    return ax, ay, ab
 
 
 def nbody_accel_f32_omp(ext, sx, sy, t0=0, nt=None, threads=0):

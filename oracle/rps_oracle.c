@@ -497,6 +497,35 @@ void orc_nbody_accel(const rps_ext_config* ext, const float* sx, const float* sy
   }
 }
 
+/* The same f64 reference for targets [t0, t0 + nt) plus, per target, the scale of f32
+ * summation error where the net force cancels: abs_sum[ii] = G * sum_j |f_ij| (f64).  Targets
+ * are independent and each sums its sources in index order, so the OpenMP build (targets over
+ * threads) returns the same bits as the serial one; used by the full-size N-body tests, whose
+ * 2^27-source sums would take minutes on one core. */
+void orc_nbody_accel_ref(const rps_ext_config* ext, const float* sx, const float* sy, uint64_t ns,
+                         uint64_t t0, uint64_t nt, float* ax, float* ay, double* abs_sum) {
+  const float eps2 = ext->nbody_softening * ext->nbody_softening;
+  const float gm = ext->nbody_strength;
+#pragma omp parallel for schedule(dynamic, 1)
+  for (uint64_t ii = 0; ii < nt; ++ii) {
+    const float xi = sx[t0 + ii], yi = sy[t0 + ii];
+    double accx = 0.0, accy = 0.0, acca = 0.0;
+    for (uint64_t j = 0; j < ns; ++j) {
+      double dx = (double)sx[j] - xi, dy = (double)sy[j] - yi;
+      double d2 = dx * dx + dy * dy;
+      double r2 = d2 + (double)eps2;
+      double inv = 1.0 / sqrt(r2);
+      double s = inv * inv * inv;
+      accx += dx * s;
+      accy += dy * s;
+      acca += sqrt(d2) * s;
+    }
+    ax[ii] = (float)(accx * gm);
+    ay[ii] = (float)(accy * gm);
+    abs_sum[ii] = acca * (double)gm;
+  }
+}
+
 void orc_nbody_accel_f32_omp(const rps_ext_config* ext, const float* sx, const float* sy,
                              uint64_t ns, uint64_t t0, uint64_t nt, float* ax, float* ay,
                              int threads) {

@@ -78,6 +78,8 @@ void orc_init_scatter(const rps_config* cfg, const rps_ext_config* ext, uint64_t
 /* All-pairs softened gravity: acc of targets [t0, t0+nt) from all ns sources. */
 void orc_nbody_accel(const rps_ext_config* ext, const float* sx, const float* sy, uint64_t ns,
                      uint64_t t0, uint64_t nt, float* ax, float* ay);
+void orc_nbody_accel_ref(const rps_ext_config* ext, const float* sx, const float* sy, uint64_t ns,
+                         uint64_t t0, uint64_t nt, float* ax, float* ay, double* abs_sum);
 /* The same force in f32 on every host core (bench.py's all-pairs cpu_baseline only, not a
  * checker): per target an f32 sum, vectorised by `omp simd` (its own summation order). */
 void orc_nbody_accel_f32_omp(const rps_ext_config* ext, const float* sx, const float* sy,

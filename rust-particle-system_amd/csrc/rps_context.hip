@@ -52,16 +52,19 @@ struct rps_ctx {
   uint32_t P = 0;
   uint32_t sort_passes = 0, sort_launches = 0;
   uint8_t sph_batch_d = 0, sph_batch_s = 0;  // forced scan batches (0: by size)
-  uint8_t sph_xcd = 0;     // RPS_SPH_XCD at create
   SphLayoutArgs lay{};     // spatial record layout (P == N, RPS_SPH_LAYOUT != 0): arrays
   uint32_t cell_cap = 0;   // their cell capacity (0: no layout)
   bool layout_last = false;  // the last active frame used the layout (slot records in storage order)
+  bool last_frame_active = false;  // the most recent frame ran passes 4-5 (rps_sph_frame_cost)
+  unsigned long long* d_count = nullptr;  // rps_sph_frame_cost's per-workgroup counts (SPH)
   // N-body
   f2* pos_all = nullptr;
   uint64_t ns_padded = 0;
   float *ax = nullptr, *ay = nullptr;
   f2* nb_part = nullptr;  // N-body source-split partials (nb_splits x n float2)
   uint32_t nb_splits = 0;  // source splits of the force launch (RPS_NBODY_SPLITS overrides)
+  uint64_t* nb_stamps = nullptr;  // profiled force launches: per-workgroup clock stamps
+  uint64_t nb_stamp_wgs = 0;      // workgroups of the last stamped launch (0: none yet)
   // device config (rps_set_config writes it on the stream: config_store_kernel)
   rps_config* d_cfg = nullptr;
   // stats
@@ -83,10 +86,7 @@ struct rps_ctx {
   bool profile_open = false;
   std::vector<hipEvent_t> ev_start, ev_stop;
   size_t ev_used = 0;
-  // tuning
-  uint32_t stream_grid = 0;  // 0: one-shot grid
-  int nontemporal = 3;
-  uint32_t xcd_order = 0;
+  int nontemporal = 3;  // stream cache policy (stream_nt_default)
   // comm
   ncclComm_t comm = nullptr;
   int rank = 0, nranks = 1;
@@ -237,7 +237,6 @@ StreamArgs make_stream_args(const rps_ctx* ctx, uint64_t k) {
   a.key1 = (uint32_t)(e.seed >> 32);
   a.step_lo = (uint32_t)k;
   a.step_hi = (uint32_t)(k >> 32);
-  a.xcd_order = ctx->xcd_order;
   return a;
 }
 
@@ -291,7 +290,6 @@ SphBuffers sph_buffers(rps_ctx* ctx) {
   b.p = ctx->P;
   b.batch_d = ctx->sph_batch_d;
   b.batch_s = ctx->sph_batch_s;
-  b.xcd_mode = ctx->sph_xcd;
   b.lay = ctx->lay;
   b.cell_cap = ctx->cell_cap;
   b.layout = ctx->layout_last;
@@ -322,8 +320,7 @@ int step_stream(rps_ctx* ctx) {
   l.lifetime = (e.flags & RPS_EXT_LIFETIME) != 0;
   l.stats = stats;
   l.nontemporal = ctx->nontemporal;
-  const uint32_t oneshot = stream_blocks_for(ctx->n);
-  l.grid = ctx->stream_grid ? std::min(ctx->stream_grid, oneshot) : oneshot;
+  l.grid = stream_blocks_for(ctx->n);
   if (stats && l.grid > ctx->partial_cap) {
     if (ctx->partials) RPS_HIP(ctx, hipFree(ctx->partials));
     ctx->partials = nullptr;
@@ -367,8 +364,7 @@ int step_stream_fused(rps_ctx* ctx, uint64_t k0, uint32_t m, bool stats, uint64_
   l.lifetime = (e.flags & RPS_EXT_LIFETIME) != 0;
   l.stats = stats;
   l.nontemporal = 3;
-  const uint32_t oneshot = stream_blocks_for(ctx->n);
-  l.grid = ctx->stream_grid ? std::min(ctx->stream_grid, oneshot) : oneshot;
+  l.grid = stream_blocks_for(ctx->n);
   if (stats && l.grid > ctx->partial_cap) {
     if (ctx->partials) RPS_HIP(ctx, hipFree(ctx->partials));
     ctx->partials = nullptr;
@@ -410,9 +406,11 @@ int step_nbody(rps_ctx* ctx) {
   const float eps2 = e.nbody_softening * e.nbody_softening;
   int rc = prof_begin(ctx);
   if (rc) return rc;
+  uint64_t* stamps = ctx->profile_open ? ctx->nb_stamps : nullptr;
   RPS_HIP(ctx, launch_nbody_accel(ctx->pos_all, ctx->ns_padded, ctx->id_offset, ctx->n, eps2,
                                   e.nbody_strength, ctx->nb_part, ctx->nb_splits, ctx->ax, ctx->ay,
-                                  ctx->stream));
+                                  stamps, ctx->stream));
+  if (stamps) ctx->nb_stamp_wgs = nbody_workgroups(ctx->n, ctx->ns_padded, ctx->nb_splits);
   rc = prof_end(ctx);
   if (rc) return rc;
   NbodyIntegrateArgs ia;
@@ -438,22 +436,22 @@ int step_nbody(rps_ctx* ctx) {
 }
 
 // Passes 1-3.  On an active frame the offsets pass (3) rides in pass 4's first kernel
-// instead (fold_offsets): nothing between them reads offsets/ends.
-int step_sph_grid(rps_ctx* ctx, bool fold_offsets) {
+// instead (the layout's runs kernel, or predict): nothing between them reads offsets/ends.
+int step_sph_grid(rps_ctx* ctx, bool active) {
   SphBuffers b = sph_buffers(ctx);
   RPS_HIP(ctx, launch_sph_sort(b, ctx->stream, &ctx->sort_passes, &ctx->sort_launches));
-  if (!fold_offsets) RPS_HIP(ctx, launch_sph_offsets(b, ctx->stream));
+  if (!active) RPS_HIP(ctx, launch_sph_offsets(b, ctx->stream));
   return RPS_OK;
 }
 
-int step_sph_sim(rps_ctx* ctx, bool with_offsets, bool layout, const SphGrid& g) {
+int step_sph_sim(rps_ctx* ctx, bool layout, const SphGrid& g) {
   ctx->layout_last = layout;
+  if (layout) ctx->lay.g = g;
   SphBuffers b = sph_buffers(ctx);
-  b.lay.g = g;
   if (layout)
     RPS_HIP(ctx, launch_sph_layout_pre(b, ctx->stream));
   else
-    RPS_HIP(ctx, launch_sph_pre(b, ctx->stream, with_offsets));
+    RPS_HIP(ctx, launch_sph_pre(b, ctx->stream));
   int rc = prof_begin(ctx);
   if (rc) return rc;
   RPS_HIP(ctx, launch_sph_sim(b, ctx->stream));
@@ -523,16 +521,12 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
   ctx->id_offset = info->id_offset;
   ctx->global_count = global;
   ctx->ext = default_ext();
-  ctx->stream_grid = (uint32_t)std::max(0, env_int("RPS_STREAM_GRID", 0));
-  ctx->nontemporal = env_int("RPS_STREAM_NT", stream_nt_default(ctx->n)) & 3;
-  ctx->xcd_order = env_int("RPS_STREAM_XCD", 0) != 0;  // measured slower
-  // Tuning knobs read per context (A/B sweeps, and tests that force a variant at small N).
+  ctx->nontemporal = stream_nt_default(ctx->n);
+  // Forced scan batches, read per context (tests force each variant at small N).
   {
     const int both = env_int("RPS_SPH_BATCH", 0);
     ctx->sph_batch_d = (uint8_t)std::max(0, std::min(255, env_int("RPS_SPH_BATCH_D", both)));
     ctx->sph_batch_s = (uint8_t)std::max(0, std::min(255, env_int("RPS_SPH_BATCH_S", both)));
-    // RPS_SPH_XCD (XCD-banded scan workgroups) is per context too, read here like the batches.
-    ctx->sph_xcd = (uint8_t)std::max(0, std::min(2, env_int("RPS_SPH_XCD", 0)));
   }
 
   auto bail = [&](int code) {
@@ -584,6 +578,7 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     slots.push_back({(void**)&ctx->offsets, align_up(n * sizeof(uint32_t), 256)});
     slots.push_back({(void**)&ctx->dens, align_up(n * sizeof(f2), 256)});
     slots.push_back({(void**)&ctx->pred, align_up(n * sizeof(f2), 256)});
+    slots.push_back({(void**)&ctx->d_count, align_up(2 * sph_count_blocks(ctx->P) * sizeof(unsigned long long), 256)});
     // Spatial record layout (rps_kernels.hip): RPS_SPH_LAYOUT=0 off, 1 (default) from 2^21
     // particles, where it is measured faster (2^22 frame 1.212 -> 1.121 ms, 2^21 0.633 ->
     // 0.609; 2^20 0.385 -> 0.391 and 2^18 0.166 -> 0.176 slower: DESIGN.md §5), 2 at any P == N.
@@ -596,8 +591,8 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
       slots.push_back({(void**)&ctx->lay.cell_info, align_up(cap * 2 * sizeof(uint4), 256)});
       slots.push_back({(void**)&ctx->lay.cellrun, align_up(cap * sizeof(uint2), 256)});
       slots.push_back({(void**)&ctx->lay.run2, align_up(n * sizeof(uint2), 256)});
-      slots.push_back({(void**)&ctx->lay.part, align_up((cap / 256 + 1) * sizeof(uint32_t), 256)});
-      slots.push_back({(void**)&ctx->lay.out_keys, align_up(n * sizeof(uint32_t), 256)});
+      slots.push_back({(void**)&ctx->lay.part, align_up((cap / 256 + 2) * sizeof(uint32_t), 256)});
+      slots.push_back({(void**)&ctx->lay.out_runs, align_up(n * sizeof(uint2), 256)});
       slots.push_back({(void**)&ctx->lay.n_out, 256});
     }
   }
@@ -630,6 +625,8 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
   if (ctx->mode == RPS_MODE_SPH) {
     ctx->layout = sph_layout();
     set_sph_fields(ctx);
+    // A layout frame does not run pass 3, so its run ends go to the key-indexed ends array.
+    if (ctx->cell_cap) ctx->lay.run_end = ctx->ends;
   }
   if (ctx->mode == RPS_MODE_STREAM) {
     ctx->layout = tiled_layout();
@@ -666,6 +663,7 @@ int rps_destroy(rps_ctx* ctx) {
   for (auto ev : ctx->ev_start) (void)hipEventDestroy(ev);
   for (auto ev : ctx->ev_stop) (void)hipEventDestroy(ev);
   if (ctx->d_staging) (void)hipFree(ctx->d_staging);
+  if (ctx->nb_stamps) (void)hipFree(ctx->nb_stamps);
   if (ctx->partials) (void)hipFree(ctx->partials);
   if (ctx->arena) (void)hipFree(ctx->arena);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -940,9 +938,10 @@ int rps_step(rps_ctx* ctx, uint32_t nsteps) {
     if (ctx->mode == RPS_MODE_SPH) {
       // passes 1-3 run every frame (particle_compute.rs:105-163); on an active frame the
       // offsets pass rides in the next kernel (the layout's runs kernel or predict)
-      rc = step_sph_grid(ctx, active && (layout || sph_fold_offsets()));
+      rc = step_sph_grid(ctx, active);
       if (rc) return rc;
     }
+    if (ctx->mode == RPS_MODE_SPH) ctx->last_frame_active = active;
     if (!active) continue;
     if (fused) {
       const uint64_t k = ctx->active_steps;
@@ -965,7 +964,7 @@ int rps_step(rps_ctx* ctx, uint32_t nsteps) {
     switch (ctx->mode) {
       case RPS_MODE_STREAM: rc = step_stream(ctx); break;
       case RPS_MODE_NBODY: rc = step_nbody(ctx); break;
-      default: rc = step_sph_sim(ctx, sph_fold_offsets(), layout, grid); break;
+      default: rc = step_sph_sim(ctx, layout, grid); break;
     }
     if (rc) return rc;
     ++ctx->active_steps;
@@ -1030,6 +1029,28 @@ int rps_set_profiling(rps_ctx* ctx, int enable) {
   ctx->profile_every = (uint32_t)enable;
   ctx->profile_seq = 0;
   ctx->ev_used = 0;
+  if (enable && ctx->mode == RPS_MODE_NBODY && !ctx->nb_stamps)
+    RPS_HIP(ctx, hipMalloc(&ctx->nb_stamps, 16 * nbody_workgroups(ctx->n, ctx->ns_padded, ctx->nb_splits)));
+  return RPS_OK;
+}
+
+int rps_get_kernel_clock(rps_ctx* ctx, double* mhz, uint64_t* workgroups) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (ctx->mode != RPS_MODE_NBODY) return fail(ctx, RPS_ERR_UNSUPPORTED, "N-body mode only");
+  if (!ctx->nb_stamp_wgs) return fail(ctx, RPS_ERR_UNSUPPORTED, "no profiled force launch yet (rps_set_profiling)");
+  std::vector<uint64_t> h(2 * ctx->nb_stamp_wgs);
+  RPS_HIP(ctx, hipMemcpyAsync(h.data(), ctx->nb_stamps, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                              ctx->stream));
+  RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  std::vector<double> clk;
+  clk.reserve(ctx->nb_stamp_wgs);
+  for (uint64_t w = 0; w < ctx->nb_stamp_wgs; ++w)
+    if (h[2 * w + 1] > 0) clk.push_back((double)h[2 * w] / (double)h[2 * w + 1] * 100.0);  // 100-MHz ticks
+  if (clk.empty()) return fail(ctx, RPS_ERR_DEVICE, "no clock stamps recorded");
+  std::nth_element(clk.begin(), clk.begin() + clk.size() / 2, clk.end());
+  if (mhz) *mhz = clk[clk.size() / 2];
+  if (workgroups) *workgroups = clk.size();
   return RPS_OK;
 }
 
@@ -1078,16 +1099,17 @@ static int sph_frame_cost(rps_ctx* ctx, rps_sph_cost* out) {
   if (ctx->mode != RPS_MODE_SPH) return fail(ctx, RPS_ERR_UNSUPPORTED, "SPH mode only");
   if (!ctx->have_config) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "rps_set_config first");
   const SphBuffers b = sph_buffers(ctx);
-  // The counts read the last active frame's lookup, runs and predicted positions.
-  if (!ctx->active_steps) return fail(ctx, RPS_ERR_UNSUPPORTED, "run an active SPH frame first");
+  // The counts read the frame's sorted lookup, runs and predicted positions: they describe the
+  // most recent frame only if that frame was active (a gated frame re-sorts the lookup and
+  // resets the runs, but leaves the previous frame's predictions).
+  if (!ctx->last_frame_active)
+    return fail(ctx, RPS_ERR_UNSUPPORTED, "the most recent SPH frame was not active (run an active frame first)");
   const uint32_t nb = sph_count_blocks(ctx->P);
-  unsigned long long* d = nullptr;
-  RPS_HIP(ctx, hipMalloc(&d, sizeof(unsigned long long) * 2 * nb));
   std::vector<unsigned long long> h(2 * (size_t)nb);
-  hipError_t e = launch_sph_count(b, d, ctx->stream);
-  if (e == hipSuccess) e = hipMemcpyAsync(h.data(), d, h.size() * sizeof(h[0]), hipMemcpyDeviceToHost, ctx->stream);
+  hipError_t e = launch_sph_count(b, ctx->d_count, ctx->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(h.data(), ctx->d_count, h.size() * sizeof(h[0]), hipMemcpyDeviceToHost, ctx->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-  (void)hipFree(d);
   if (e != hipSuccess) return fail(ctx, RPS_ERR_DEVICE, std::string("SPH cost count: ") + hipGetErrorString(e));
   uint64_t E = 0, W = 0;
   for (uint32_t i = 0; i < nb; ++i) {
@@ -1110,9 +1132,8 @@ static int sph_frame_cost(rps_ctx* ctx, rps_sph_cost* out) {
 
 int rps_sph_frame_cost(rps_ctx* ctx, rps_sph_cost* out) { return sph_frame_cost(ctx, out); }
 
-int rps_step_cost(const rps_ctx* cctx, double* amount, int* unit) {
-  if (!cctx || !amount || !unit) return fail(nullptr, RPS_ERR_INVALID_ARGUMENT, "null argument");
-  rps_ctx* ctx = const_cast<rps_ctx*>(cctx);  // SPH counts on the device (no state change)
+int rps_step_cost(rps_ctx* ctx, double* amount, int* unit) {
+  if (!ctx || !amount || !unit) return fail(nullptr, RPS_ERR_INVALID_ARGUMENT, "null argument");
   switch (ctx->mode) {
     case RPS_MODE_STREAM: {
       // r+w of x, y, vx, vy (+ the group's u16 [next] read, 2 B per 64 particles; the expiry

@@ -126,7 +126,6 @@ struct StreamArgs {
   float emit_cx, emit_cy, emit_r, spd_min, spd_range, life_min, life_range;
   uint32_t key0, key1, step_lo, step_hi;
   uint32_t clock;      // lifetime clock of this step (low 16 bits compared with the expiry)
-  uint32_t xcd_order;  // 1: workgroup b takes block xcd_block(b) (contiguous range per XCD)
 };
 
 // Temporal fusion of up to kMaxFuse consecutive active steps in one launch: per-substep

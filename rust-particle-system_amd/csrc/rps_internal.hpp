@@ -75,9 +75,13 @@ constexpr uint32_t kNbodyMaxSplits = 64;
 uint32_t nbody_splits_for(uint64_t nt, uint64_t ns_padded);
 // `splits` source splits (1: the kernel writes the accelerations directly; > 1: each split
 // writes nt float2 partials into `part` and a fixed-order reduce follows).
+// stamps (nullable): per workgroup {shader cycles, 100-MHz ticks} of its lifetime (16 B each,
+// nbody_workgroups(nt, ns_padded, splits) of them), for the sustained-clock report of
+// profiled launches.
 hipError_t launch_nbody_accel(const f2* pos, uint64_t ns_padded, uint64_t t0, uint64_t nt,
                               float eps2, float gm, f2* part, uint32_t splits, float* ax,
-                              float* ay, hipStream_t s);
+                              float* ay, uint64_t* stamps, hipStream_t s);
+uint64_t nbody_workgroups(uint64_t nt, uint64_t ns_padded, uint32_t splits);
 struct NbodyIntegrateArgs {
   float* x;
   float* y;
@@ -116,9 +120,11 @@ struct SphLayoutArgs {
                        //   owns (length 0: none)
   uint2* cellrun;      // cells: storage {start, end} of the cell's key's run (start >= N: none)
   uint2* run2;         // N: storage {start, end} per key ({0xFFFFFFFF, 0}: none; reset in bin)
-  uint32_t* part;      // cells / 256 + 1: 256-cell block sums -> bases (0 between frames)
-  uint32_t* out_keys;  // N: keys of runs placed after the grid's
+  uint32_t* part;      // cells / 256 + 2: 256-cell block sums -> bases; [blocks]: the grid's
+                       //   total (the listed runs' storage starts there)
+  uint2* out_runs;     // N: {first slot, storage base} of the runs placed after the grid's
   uint32_t* n_out;     // 1: their count (0 between frames)
+  uint32_t* run_end;   // N: one past the last slot of each key's run (the runs kernel)
 };
 struct SphBuffers {
   const rps_config* cfg;  // device-resident ParticleConfig
@@ -133,7 +139,6 @@ struct SphBuffers {
   uint32_t p;        // next_pow2(N)
   uint8_t batch_d;   // scan entries in flight per lane, density / sim pass (4, 8, 16;
   uint8_t batch_s;   //   0: by size, sph_batch); per context, RPS_SPH_BATCH[_D|_S] at create
-  uint8_t xcd_mode;  // RPS_SPH_XCD at create: 0 off, 1 with the layout, 2 always
   bool layout;       // this frame uses the spatial record layout (lay.* valid, P == N)
   uint32_t cell_cap; // capacity of lay.cell_info / cellrun (0: layout never available)
   SphLayoutArgs lay;
@@ -150,10 +155,10 @@ int sph_batch(bool density, uint32_t p, int forced, bool layout);
 hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
                            uint32_t* launches);
 hipError_t launch_sph_offsets(const SphBuffers& b, hipStream_t s);
-// with_offsets: the predict kernel also runs the offsets pass (it needs only the sorted
-// lookup), saving a launch on active frames; see sph_fold_offsets (RPS_SPH_FOLD_OFFSETS=0: off).
-hipError_t launch_sph_pre(const SphBuffers& b, hipStream_t s, bool with_offsets);
-bool sph_fold_offsets();
+// Active-frame passes 3-4 without the layout: the predict kernel also runs the offsets pass
+// (it needs only the sorted lookup; one launch fewer: 65 536 0.1118 -> 0.1105 ms/frame), then
+// density.
+hipError_t launch_sph_pre(const SphBuffers& b, hipStream_t s);
 hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s);
 // Cost accounting (rps_sph_frame_cost): per workgroup of slots, the (scanned, within-radius)
 // neighbour entries of the current frame, as u64 pairs in out[2 * sph_count_blocks(p)].

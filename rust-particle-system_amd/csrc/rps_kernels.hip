@@ -144,16 +144,8 @@ __device__ void block_reduce_stats(StatsAcc acc, StatsPartial* out) {
 // respawn, only when one is due: 32.03 B per particle plus ~19 % of groups' expiry lines at
 // C3.
 // ---------------------------------------------------------------------------------------
-// NTM: bit 0 = nontemporal loads, bit 1 = nontemporal stores.
-// Workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, "Workgroup
-// dispatch"): with xcd_order, workgroup b takes block x*q + min(x, r) + b/8 (x = b % 8,
-// q = G/8, r = G%8), a bijection that gives each XCD one contiguous range of tiles.
-// Speed only; every particle is still visited exactly once.
-__device__ __forceinline__ uint64_t stream_block(const StreamArgs& a, uint32_t b) {
-  if (!a.xcd_order) return b;
-  const uint32_t G = gridDim.x, q = G / 8, r = G % 8, x = b % 8, k = b / 8;
-  return (uint64_t)x * q + (x < r ? x : r) + k;
-}
+// NTM: bit 0 = nontemporal loads, bit 1 = nontemporal stores.  Workgroup b takes block b: an
+// XCD-contiguous numbering (each XCD one range of tiles) was measured 3 % slower.
 
 // The attractor table inside this launch's kernarg segment (see StreamArgs::att).
 template <class Args>
@@ -259,7 +251,7 @@ __device__ __forceinline__ void stream_body(const StreamArgs& a, att_ptr att0, s
   constexpr bool NTL = (NTM & 1) != 0, NTS = (NTM & 2) != 0;
   const uint64_t nvec = a.n >> 2;
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-  const uint64_t tid = stream_block(a, blockIdx.x) * kBlock + threadIdx.x;
+  const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   const uint64_t step0 = ((uint64_t)a.step_hi << 32) | a.step_lo;
   StatsAcc acc;
   if constexpr (STATS) acc.init();
@@ -983,17 +975,6 @@ __device__ __forceinline__ bool grid_cell(const SphGrid& g, uint32_t e, int32_t&
   return x < g.w && y < g.h;
 }
 
-// Workgroup -> chunk of the launch's index range.  xcd != 0: workgroups are dealt round-robin
-// over the 8 XCDs (MI355X_MICROARCH.md, dispatch), so workgroup b takes chunk
-// (b % 8) * (nb / 8) + ...: each XCD walks one contiguous eighth of the range, and with the
-// spatial record layout one spatial band whose records stay in that XCD's L2.
-__device__ __forceinline__ uint32_t wg_index(uint32_t xcd) {
-  const uint32_t b = blockIdx.x;
-  if (!xcd) return b;
-  const uint32_t nb = gridDim.x, x = b & 7u, q = nb >> 3, r = nb & 7u;
-  return x * q + min(x, r) + (b >> 3);
-}
-
 __constant__ int32_t kGridOff[9][2] = {{-1, -1}, {-1, 0}, {-1, 1}, {0, -1}, {0, 0},
                                        {0, 1},   {1, -1}, {1, 0},  {1, 1}};
 
@@ -1159,9 +1140,8 @@ struct RunCursor {
 // predicted positions in flight per lane across run boundaries.
 template <int kScanBatch, bool LAYOUT>
 __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* __restrict__ cfg,
-                                                             RunBounds rb, SphSlots sl, uint32_t p_slots,
-                                                             uint32_t xcd) {
-  const uint32_t t = wg_index(xcd) * kBlock + threadIdx.x;
+                                                             RunBounds rb, SphSlots sl, uint32_t p_slots) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= p_slots) return;
   const f2 p = sl.pp_s[t];
   const float r = cfg->smoothing_radius, r2 = r * r;
@@ -1289,8 +1269,8 @@ __device__ __forceinline__ void scan_runs(const SphSlots& sl, const RunTable& ru
 template <int kScanBatch, bool kPads, bool LAYOUT>
 __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __restrict__ cfg,
                                                          RunBounds rb, SphSlots sl, f4* __restrict__ st,
-                                                         uint32_t p_slots, uint32_t xcd) {
-  const uint32_t t = wg_index(xcd) * kBlock + threadIdx.x;
+                                                         uint32_t p_slots) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= p_slots) return;
   const f4 own = sl.rec_pd[t];  // own predicted position (xy) and P / rho^2 (z)
   const f2 own_d = sl.dens_s[t];
@@ -1479,7 +1459,9 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* t
 }
 
 // Each run's length and owner cell (the layout's replacement for pass 3: the scans find runs
-// through cellrun / run2, and the reference's offsets are rebuilt on debug readback).
+// through cellrun / run2, and the reference's offsets are rebuilt on debug readback).  Every
+// run's last slot also records the run's end by key (run_end), so the scan kernel sizes a
+// listed run with one load whatever its length.
 __global__ __launch_bounds__(kBlock) void sph_runs_kernel(SphLayoutArgs a, const rps_config* __restrict__ cfg,
                                                           const uint2* __restrict__ lookup,
                                                           const f4* __restrict__ st, uint32_t n) {
@@ -1487,6 +1469,8 @@ __global__ __launch_bounds__(kBlock) void sph_runs_kernel(SphLayoutArgs a, const
   if (t >= n) return;
   const uint2 e = lookup[t];
   const uint32_t prev = t > 0u ? lookup[t - 1u].x : 0xFFFFFFFFu;
+  const uint32_t next = t + 1u < n ? lookup[t + 1u].x : ~e.x;
+  if (next != e.x) a.run_end[e.x] = t + 1u;
   if (e.x == prev) return;
   // The cell of the run's first particle, computed as the bin pass did (same state, same
   // ops), so its key is e.x; anything else (never seen) is handled as outside the grid.
@@ -1513,7 +1497,7 @@ __global__ __launch_bounds__(kBlock) void sph_runs_kernel(SphLayoutArgs a, const
   const int32_t cy = f32_to_i32((s[1] + cfg->screen_bounds[3]) / r);
   const uint32_t c = cell_key(cx, cy, cfg->particle_count) == e.x ? grid_enum(a.g, cx, cy) : kCellOut;
   if (c == kCellOut || len > kRunScan) {
-    a.out_keys[atomicAdd(a.n_out, 1u)] = t;  // placed by the scan kernel
+    a.out_runs[atomicAdd(a.n_out, 1u)] = make_uint2(t, 0u);  // placed by the scan kernel
   } else {
     a.cell_info[2u * c] = make_uint4(t, len, idx[0], idx[1]);
     a.cell_info[2u * c + 1u] = make_uint4(idx[2], idx[3], idx[4], idx[5]);
@@ -1529,11 +1513,13 @@ __global__ __launch_bounds__(kBlock) void sph_layout_count_kernel(SphLayoutArgs 
   if (threadIdx.x == 0) a.part[blockIdx.x] = tot;
 }
 
+// Block bases from the block sums (one workgroup), then the listed runs (first particle
+// outside the grid, or longer than kRunScan) after the grid's, in list order: each one's
+// length from run_end, its storage run (run2) and base (out_runs[j].y).  part[nparts] gets the
+// grid's total, where the listed runs' storage starts; the write kernel predicts their slots.
 __global__ __launch_bounds__(1024) void sph_layout_scan_kernel(SphLayoutArgs a,
-                                                               const rps_config* __restrict__ cfg,
                                                                const uint2* __restrict__ lookup,
-                                                               const f4* __restrict__ st, SphSlots sl,
-                                                               uint32_t nparts, uint32_t n) {
+                                                               uint32_t nparts) {
   const uint32_t m = *a.n_out;
   const uint32_t per = (nparts + 1023u) / 1024u, b0 = threadIdx.x * per;
   uint32_t sum = 0;
@@ -1547,28 +1533,24 @@ __global__ __launch_bounds__(1024) void sph_layout_scan_kernel(SphLayoutArgs a,
       a.part[b0 + k] = pre;
       pre += v;
     }
-  // The listed runs (first particle outside the grid, or longer than kRunScan), after the
-  // grid's, in list order.
+  if (threadIdx.x == 0) a.part[nparts] = total;
   uint32_t base = total;
   for (uint32_t c = 0; c < m; c += 1024u) {
     const uint32_t j = c + threadIdx.x;
     uint32_t key = 0, t = 0, len = 0;
     if (j < m) {
-      t = a.out_keys[j];
+      t = a.out_runs[j].x;
       key = lookup[t].x;
-      len = 1;
-      while (t + len < n && lookup[t + len].x == key) ++len;
+      len = a.run_end[key] - t;
     }
     uint32_t tot;
     const uint32_t p = base + block_exclusive_scan<1024>(len, &tot);
     if (j < m) {
       a.run2[key] = make_uint2(p, p + len);
-      for (uint32_t r = 0; r < len; ++r) predict_slot(cfg, st, sl, p + r, lookup[t + r].y);
+      a.out_runs[j] = make_uint2(t, p);
     }
     base += tot;
   }
-  __syncthreads();
-  if (threadIdx.x == 0) *a.n_out = 0u;  // for the next frame's runs kernel
 }
 
 // Storage runs of a block of 256 cells, and pass 4's prediction (predict_slot) for the
@@ -1629,11 +1611,28 @@ __global__ __launch_bounds__(kBlock) void sph_layout_write_kernel(SphLayoutArgs 
     const uint32_t i = r < kRunIdx ? lidx[r][lo] : lookup[lsrc[lo] + r].y;
     predict_slot(cfg, st, sl, b0 + k, i);
   }
+  // The listed runs' slots [part[blocks], N), spread over every thread of the launch (one slot
+  // per thread at most once the launch covers N: a clump of many particles in one run costs
+  // no lane more than its share); the run of slot k by binary search over their bases.
+  const uint32_t m = *a.n_out;
+  const uint32_t stride = gridDim.x * kBlock;
+  for (uint32_t k = a.part[gridDim.x] + blockIdx.x * kBlock + threadIdx.x; k < N; k += stride) {
+    uint32_t lo = 0, hi = m;  // the last listed run whose base is <= k
+    while (hi - lo > 1u) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (a.out_runs[mid].y <= k) lo = mid;
+      else hi = mid;
+    }
+    const uint2 run = a.out_runs[lo];
+    predict_slot(cfg, st, sl, k, lookup[run.x + (k - run.y)].y);
+  }
 }
 
 // Cells owning no run take their key's storage run from run2 (complete after the write pass).
+// The listed-run count goes back to 0 for the next frame's runs kernel.
 __global__ __launch_bounds__(kBlock) void sph_layout_fixup_kernel(SphLayoutArgs a, uint32_t N) {
   const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+  if (c == 0u) *a.n_out = 0u;
   if (c >= a.g.cells) return;
   if (a.cellrun[c].x == kCellPending) {
     int32_t cx, cy;
@@ -1670,24 +1669,17 @@ static hipError_t launch_stream_t(const StreamArgs& a, uint32_t grid, hipStream_
   // tools/ab_stream.py, AB_LIFE=0): 8 waves 0.5051 ms, 7 0.5004, 6 0.4767, 5 0.4766, 4
   // 0.4854.  The C3 kernel (71 VGPRs, 7 waves) is unchanged at 6 (0.4923 vs 0.4924) and
   // slower at 5 (0.5050) and 4 (0.5358); the stats steps (83-91 VGPRs) run 5 either way.
-  // RPS_STREAM_LDS=<bytes> overrides it (0 = no cap).
-  static const uint32_t lds = [] {
-    const char* v = std::getenv("RPS_STREAM_LDS");
-    const long k = v && *v ? std::atol(v) : 25000;
-    return (uint32_t)(k < 0 ? 0 : (k > 65536 ? 65536 : k));
-  }();
-  hipLaunchKernelGGL((stream_step_kernel<V, L, S, NTM>), dim3(grid), dim3(kBlock), lds, s, a);
+  constexpr uint32_t kStreamLds = 25000;
+  hipLaunchKernelGGL((stream_step_kernel<V, L, S, NTM>), dim3(grid), dim3(kBlock), kStreamLds, s, a);
   return hipGetLastError();
 }
 
+// Cache policy (stream_nt_default, rps_context.hip): nontemporal stores always; nontemporal
+// loads (3) or temporal loads (2, states of 48-576 MiB, which the Infinity Cache partly serves).
 template <bool V, bool L, bool S>
 static hipError_t launch_stream_nt(const StreamArgs& a, const StreamLaunch& l, hipStream_t s) {
-  switch (l.nontemporal & 3) {
-    case 0: return launch_stream_t<V, L, S, 0>(a, l.grid, s);
-    case 1: return launch_stream_t<V, L, S, 1>(a, l.grid, s);
-    case 2: return launch_stream_t<V, L, S, 2>(a, l.grid, s);
-    default: return launch_stream_t<V, L, S, 3>(a, l.grid, s);
-  }
+  if (l.nontemporal == 2) return launch_stream_t<V, L, S, 2>(a, l.grid, s);
+  return launch_stream_t<V, L, S, 3>(a, l.grid, s);
 }
 
 hipError_t launch_stream_step(const StreamArgs& a, const StreamLaunch& l, hipStream_t s) {
@@ -1845,22 +1837,15 @@ static hipError_t launch_sort_local(int kmax, bool bin, uint32_t tiles, uint32_t
   else                                                                                           \
     hipLaunchKernelGGL((sph_sort_local_kernel<B, K>), dim3(tiles), dim3(threads), 0, s, lookup,  \
                        tile, lo, hi, first, sb, vec)
-  // 16-B tile loads/stores (RPS_SORT_VEC=0: 8-B, one entry per lane).
-  static const uint32_t vec_env = [] {
-    const char* v = std::getenv("RPS_SORT_VEC");
-    return (v && *v) ? (uint32_t)(std::atoi(v) != 0) : 1u;
-  }();
-  const uint32_t vec = (tile >= 2u) ? vec_env : 0u;
+  // 16-B tile loads/stores, two entries per lane (8-B ones: 65 536 0.1157 -> 0.112 ms/frame,
+  // 2^19 -1.3 %); a one-entry tile (P == 1) takes the 8-B path.
+  const uint32_t vec = tile >= 2u ? 1u : 0u;
   if (bin) {
-    if (kmax == 4) RPS_LOCAL(true, 4);
-    else if (kmax == 3) RPS_LOCAL(true, 3);
-    else if (kmax == 2) RPS_LOCAL(true, 2);
-    else RPS_LOCAL(true, 1);
+    if (kmax == 3) RPS_LOCAL(true, 3);
+    else RPS_LOCAL(true, 2);
   } else {
-    if (kmax == 4) RPS_LOCAL(false, 4);
-    else if (kmax == 3) RPS_LOCAL(false, 3);
-    else if (kmax == 2) RPS_LOCAL(false, 2);
-    else RPS_LOCAL(false, 1);
+    if (kmax == 3) RPS_LOCAL(false, 3);
+    else RPS_LOCAL(false, 2);
   }
 #undef RPS_LOCAL
   return hipGetLastError();
@@ -1874,11 +1859,6 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
   while ((1u << stages) < P) ++stages;
   *passes = stages * (stages + 1u) / 2u;
   *launches = 0;
-  static const int kmax_env = [] {
-    const char* v = std::getenv("RPS_SORT_KMAX");
-    const int k = v && *v ? std::atoi(v) : 0;  // 0: by tile size (below)
-    return k < 0 ? 0 : (k > 4 ? 4 : k);
-  }();
   const SortBin bin{b.cfg, b.st, b.offsets, b.n, b.lay.run2};
   const SortBin nobin{nullptr, nullptr, nullptr, 0u, nullptr};
   if (stages == 0) {  // P == 1: nothing to sort, only bin
@@ -1889,72 +1869,41 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
   }
   // Tile: P / 256 entries clamped to [2048, 8192] -- one workgroup per CU in the LDS passes
   // once P allows it, and the largest such tile (fewest global passes).  Measured per size
-  // (tools/kmax_sweep.sh): 2048 up to P = 2^19, 4096 at 2^20, 8192 from 2^21.
-  // A fixed 8192 above 2^18 left half the CUs idle at 2^20 (0.429 -> 0.404 ms/frame) and
-  // 2^19 (0.294 -> 0.265).
-  static const uint32_t tile_env = [] {
-    const char* v = std::getenv("RPS_SORT_TILE");
-    const uint32_t t = v && *v ? (uint32_t)std::atoi(v) : 0u;
-    return (t >= 64u && t <= kSortTileMax && (t & (t - 1u)) == 0u) ? t : 0u;
-  }();
-  static const uint32_t fuse = [] {
-    const char* v = std::getenv("RPS_SORT_FUSE");
-    const int k = v && *v ? std::atoi(v) : 4;
-    return (uint32_t)(k < 1 ? 1 : (k > 5 ? 5 : k));
-  }();
-  // Stages with at least this many global passes run them in one gathered-tile launch
-  // (sph_sort_stage_kernel); RPS_SORT_GATHER_MIN=0 turns it off.
-  static const uint32_t gather_min = [] {
-    const char* v = std::getenv("RPS_SORT_GATHER_MIN");
-    const int k = v && *v ? std::atoi(v) : 5;
-    return k <= 0 ? 100u : (uint32_t)k;
-  }();
-  const uint32_t want = tile_env ? tile_env : std::min(kSortTile, std::max(2048u, P / 256u));
-  uint32_t tile = P < want ? P : want;
+  // (DESIGN.md §5): 2048 up to P = 2^19, 4096 at 2^20, 8192 from 2^21.  A fixed 8192 above
+  // 2^18 left half the CUs idle at 2^20 (0.429 -> 0.404 ms/frame) and 2^19 (0.294 -> 0.265).
+  const uint32_t tile = std::min(P, std::min(kSortTile, std::max(2048u, P / 256u)));
   // Passes per register chunk: 3 on 8192-entry tiles, 2 on smaller ones (measured at 65 536
   // to 2^22 particles; 4 is slower everywhere: fewer waves per CU).
-  int kmax = kmax_env ? kmax_env : (tile >= kSortTile ? 3 : 2);
+  const int kmax = tile >= kSortTile ? 3 : 2;
   uint32_t tile_log = 0;
   while ((1u << tile_log) < tile) ++tile_log;
-  uint32_t tiles = P / tile;
+  const uint32_t tiles = P / tile;
   // Stages whose whole network fits one tile: one launch (with the bin pass).
   const uint32_t first_global_stage = tile_log;  // stage s has 2*2^s = 2^(s+1) span
-  uint32_t lt = std::max(64u, std::min(1024u, tile >> kmax));
+  const uint32_t lt = std::max(64u, std::min(1024u, tile >> kmax));
   hipError_t e = launch_sort_local(kmax, true, tiles, lt, s, b.lookup, tile, 0u, first_global_stage - 1u,
                                    0u, bin);
   ++*launches;
   if (e != hipSuccess) return e;
-  // Tile of the later stages' local launches (RPS_SORT_TILE2; default: the first launch's).
-  // A smaller one moves one more pass per stage into the global launches.
-  static const uint32_t tile2_env = [] {
-    const char* v = std::getenv("RPS_SORT_TILE2");
-    const uint32_t t = v && *v ? (uint32_t)std::atoi(v) : 0u;
-    return (t >= 64u && t <= kSortTileMax && (t & (t - 1u)) == 0u) ? t : 0u;
-  }();
-  if (tile2_env && tile2_env < tile) {
-    tile = tile2_env;
-    tile_log = 0;
-    while ((1u << tile_log) < tile) ++tile_log;
-    tiles = P / tile;
-    kmax = kmax_env ? kmax_env : (tile >= kSortTile ? 3 : 2);
-    lt = std::max(64u, std::min(1024u, tile >> kmax));
-  }
   for (uint32_t stage = first_global_stage; stage < stages; ++stage) {
-    // Passes whose compare span 2*gw exceeds the tile are global: steps [0, T).  They run
-    // in register-fused chunks of up to `fuse` passes (sph_sort_fused_kernel).
+    // Passes whose compare span 2*gw exceeds the tile are global: steps [0, T).  Up to four
+    // of them run as one register-fused launch (sph_sort_fused_kernel); three or five per
+    // launch were slower.
     uint32_t T = 0;
     while (T <= stage && 2u * (1u << (stage - T)) > tile) ++T;
     uint32_t step = 0;
     // Five global passes: one register-fused launch (32 entries per thread) once P gives it
     // 2^17 threads; the gathered-tile launch below otherwise (2^22 frame 1.2352 -> 1.2248 ms;
     // at 2^20 and 65 536 the fused launch is slower: 0.3852 -> 0.3882, 0.1157 -> 0.1213).
-    if (T == 5u && P >= (1u << 22) && fuse >= 4u) {
+    if (T == 5u && P >= (1u << 22)) {
       e = launch_sort_fused<5>(b.lookup, P, 1u << stage, true, s);
       ++*launches;
       if (e != hipSuccess) return e;
       step = T;
     }
-    if (step < T && T >= gather_min && T <= 9u && tile_log >= 6u) {  // all T global passes, one launch
+    // Stages with five or more global passes run them all in one gathered-tile launch
+    // (sph_sort_stage_kernel).
+    if (step < T && T >= 5u && T <= 9u && tile_log >= 6u) {
       const uint32_t tt = 32u << T;
       const uint32_t blocks = (P >> (stage + 1u)) << (tile_log - 5u);
       const uint32_t threads = std::max(64u, std::min(1024u, tt >> 3));
@@ -1970,15 +1919,14 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
       step = T;
     }
     while (step < T) {
-      const uint32_t k = T - step < fuse ? T - step : fuse;
+      const uint32_t k = T - step < 4u ? T - step : 4u;
       const uint32_t G = 1u << (stage - step);
       const bool flip = step == 0;
       switch (k) {
         case 1: e = launch_sort_fused<1>(b.lookup, P, G, flip, s); break;
         case 2: e = launch_sort_fused<2>(b.lookup, P, G, flip, s); break;
         case 3: e = launch_sort_fused<3>(b.lookup, P, G, flip, s); break;
-        case 4: e = launch_sort_fused<4>(b.lookup, P, G, flip, s); break;
-        default: e = launch_sort_fused<5>(b.lookup, P, G, flip, s); break;
+        default: e = launch_sort_fused<4>(b.lookup, P, G, flip, s); break;
       }
       ++*launches;
       if (e != hipSuccess) return e;
@@ -2015,42 +1963,19 @@ int sph_batch(bool density, uint32_t p, int forced, bool layout) {
   return p > (1u << 21) ? 6 : 4;
 }
 
-bool sph_fold_offsets() {
-  static const bool f = [] {
-    const char* v = std::getenv("RPS_SPH_FOLD_OFFSETS");
-    return !(v && *v && std::atoi(v) == 0);
-  }();
-  return f;
-}
-
-// Experiment knob: LDS bytes reserved (never used) on a scan launch, an occupancy cap.
-static uint32_t sph_lds_extra(const char* name) {
-  const char* v = std::getenv(name);
-  const long k = v && *v ? std::atol(v) : 0;
-  return (uint32_t)(k < 0 ? 0 : (k > 65536 ? 65536 : k));
-}
-
-// XCD-banded workgroups for the slot-order passes (RPS_SPH_XCD=1: with the spatial layout,
-// where a band of slots is a band of space; 2: always; default off: measured slower).
-static uint32_t sph_xcd(const SphBuffers& b) {
-  return b.xcd_mode == 2 ? 1u : (b.xcd_mode == 1 ? (uint32_t)b.layout : 0u);
-}
-
 static RunBounds run_bounds(const SphBuffers& b) {
   return RunBounds{b.offsets, b.ends, b.lay.cellrun, b.lay.run2, b.lay.g};
 }
 
 static hipError_t launch_sph_density(const SphBuffers& b, hipStream_t s) {
-  static const uint32_t lds_d = sph_lds_extra("RPS_SPH_DENSITY_LDS");
-  const uint32_t xcd = sph_xcd(b);
   const RunBounds rb = run_bounds(b);
 #define RPS_DENSITY(B)                                                                            \
   if (b.layout)                                                                                   \
-    hipLaunchKernelGGL((sph_density_kernel<B, true>), dim3(blocks_for(b.p)), dim3(kBlock), lds_d, s, \
-                       b.cfg, rb, b.sl, b.p, xcd);                                               \
+    hipLaunchKernelGGL((sph_density_kernel<B, true>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s, \
+                       b.cfg, rb, b.sl, b.p);                                               \
   else                                                                                            \
-    hipLaunchKernelGGL((sph_density_kernel<B, false>), dim3(blocks_for(b.p)), dim3(kBlock), lds_d, s, \
-                       b.cfg, rb, b.sl, b.p, xcd)
+    hipLaunchKernelGGL((sph_density_kernel<B, false>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s, \
+                       b.cfg, rb, b.sl, b.p)
   switch (sph_batch(true, b.p, b.batch_d, b.layout)) {
     case 4: RPS_DENSITY(4); break;
     case 16: RPS_DENSITY(16); break;
@@ -2060,9 +1985,9 @@ static hipError_t launch_sph_density(const SphBuffers& b, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_sph_pre(const SphBuffers& b, hipStream_t s, bool with_offsets) {
+hipError_t launch_sph_pre(const SphBuffers& b, hipStream_t s) {
   hipLaunchKernelGGL(sph_predict_kernel, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg, b.lookup, b.st,
-                     b.sl, b.p, b.offsets, b.ends, with_offsets ? b.n : 0u);
+                     b.sl, b.p, b.offsets, b.ends, b.n);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   return launch_sph_density(b, s);
@@ -2098,8 +2023,7 @@ hipError_t launch_sph_layout_pre(const SphBuffers& b, hipStream_t s) {
   const uint32_t nparts = blocks_for(a.g.cells);
   hipLaunchKernelGGL(sph_layout_count_kernel, dim3(nparts), dim3(kBlock), 0, s, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(sph_layout_scan_kernel, dim3(1), dim3(1024), 0, s, a, b.cfg, b.lookup, b.st, b.sl,
-                     nparts, b.n);
+  hipLaunchKernelGGL(sph_layout_scan_kernel, dim3(1), dim3(1024), 0, s, a, b.lookup, nparts);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(sph_layout_write_kernel, dim3(nparts), dim3(kBlock), 0, s, a, b.cfg, b.lookup, b.st,
                      b.sl, b.n);
@@ -2110,19 +2034,17 @@ hipError_t launch_sph_layout_pre(const SphBuffers& b, hipStream_t s) {
 }
 
 hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s) {
-  static const uint32_t lds_s = sph_lds_extra("RPS_SPH_SIM_LDS");
   const RunBounds rb = run_bounds(b);
-  const uint32_t xcd = sph_xcd(b);
 #define RPS_SIM(B)                                                                                  \
   if (b.layout)                                                                                     \
-    hipLaunchKernelGGL((sph_sim_kernel<B, false, true>), dim3(blocks_for(b.p)), dim3(kBlock), lds_s, s, \
-                       b.cfg, rb, b.sl, b.st, b.p, xcd);                                           \
+    hipLaunchKernelGGL((sph_sim_kernel<B, false, true>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s, \
+                       b.cfg, rb, b.sl, b.st, b.p);                                           \
   else if (b.p == b.n)                                                                              \
-    hipLaunchKernelGGL((sph_sim_kernel<B, false, false>), dim3(blocks_for(b.p)), dim3(kBlock), lds_s, s, \
-                       b.cfg, rb, b.sl, b.st, b.p, xcd);                                           \
+    hipLaunchKernelGGL((sph_sim_kernel<B, false, false>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s, \
+                       b.cfg, rb, b.sl, b.st, b.p);                                           \
   else                                                                                              \
-    hipLaunchKernelGGL((sph_sim_kernel<B, true, false>), dim3(blocks_for(b.p)), dim3(kBlock), lds_s, s, \
-                       b.cfg, rb, b.sl, b.st, b.p, xcd)
+    hipLaunchKernelGGL((sph_sim_kernel<B, true, false>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s, \
+                       b.cfg, rb, b.sl, b.st, b.p)
   switch (sph_batch(false, b.p, b.batch_s, b.layout)) {
     case 4: RPS_SIM(4); break;
     case 6: RPS_SIM(6); break;

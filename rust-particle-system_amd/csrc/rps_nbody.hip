@@ -47,8 +47,19 @@ __global__ __launch_bounds__(kBlock) void nbody_accel_kernel(const f2* __restric
                                                              uint64_t split_len,
                                                              f2* __restrict__ part,
                                                              float* __restrict__ ax_out,
-                                                             float* __restrict__ ay_out) {
+                                                             float* __restrict__ ay_out,
+                                                             uint64_t* __restrict__ stamps) {
   static_assert(kNbodyTile / 2 == kBlock, "one float2 source pair per lane per tile");
+  // Clock stamps (profiled launches only, stamps != nullptr): the workgroup's shader-clock
+  // counter and 100-MHz real-time counter at its start and end, so the host can report the
+  // clock the chip sustained under this kernel (MI355X_MICROARCH.md, DVFS: in-kernel clock =
+  // delta s_memtime / delta s_memrealtime x 100 MHz).  Two reads per workgroup lifetime
+  // (~90 ms at 2^22), written to a buffer nothing else reads; no output depends on them.
+  uint64_t c0 = 0, r0 = 0;
+  if (stamps && threadIdx.x == 0) {
+    c0 = __builtin_amdgcn_s_memtime();
+    r0 = __builtin_amdgcn_s_memrealtime();
+  }
   __shared__ f4 tile[kNbodyTile / 2];  // pairs of float2 sources
   // Two-level summation: the registers ax/ay sum one tile's 512 contributions, and each
   // lane's running totals live in LDS (tot[2p + c][lane], conflict-free 8-B accesses), added
@@ -131,6 +142,12 @@ __global__ __launch_bounds__(kBlock) void nbody_accel_kernel(const f2* __restric
       }
     }
   }
+  if (stamps && threadIdx.x == 0) {
+    const uint64_t c1 = __builtin_amdgcn_s_memtime();
+    const uint64_t r1 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t wg = (uint64_t)blockIdx.y * gridDim.x + blockIdx.x;
+    reinterpret_cast<ulonglong2*>(stamps)[wg] = make_ulonglong2(c1 - c0, r1 - r0);
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void nbody_reduce_kernel(const f2* __restrict__ part,
@@ -195,18 +212,29 @@ uint32_t nbody_splits_for(uint64_t nt, uint64_t ns_padded) {
   return s < 1 ? 1u : (uint32_t)s;
 }
 
-hipError_t launch_nbody_accel(const f2* pos, uint64_t ns_padded, uint64_t t0, uint64_t nt,
-                              float eps2, float gm, f2* part, uint32_t splits, float* ax,
-                              float* ay, hipStream_t s) {
-  if (nt == 0) return hipSuccess;
+// The split count a launch actually uses: splits of whole tiles, none of them empty.
+static uint32_t launch_splits(uint64_t ns_padded, uint32_t splits, uint64_t* split_len) {
   const uint64_t tiles = ns_padded / kNbodyTile;
   if (splits < 1) splits = 1;
   if (splits > tiles) splits = (uint32_t)tiles;
-  const uint64_t split_len = (tiles + splits - 1) / splits * kNbodyTile;
-  splits = (uint32_t)((ns_padded + split_len - 1) / split_len);  // no empty split
+  *split_len = (tiles + splits - 1) / splits * kNbodyTile;
+  return (uint32_t)((ns_padded + *split_len - 1) / *split_len);
+}
+
+uint64_t nbody_workgroups(uint64_t nt, uint64_t ns_padded, uint32_t splits) {
+  uint64_t len;
+  return (uint64_t)blocks_for(nt, kBlock * kTargetsPerLane) * launch_splits(ns_padded, splits, &len);
+}
+
+hipError_t launch_nbody_accel(const f2* pos, uint64_t ns_padded, uint64_t t0, uint64_t nt,
+                              float eps2, float gm, f2* part, uint32_t splits, float* ax,
+                              float* ay, uint64_t* stamps, hipStream_t s) {
+  if (nt == 0) return hipSuccess;
+  uint64_t split_len;
+  splits = launch_splits(ns_padded, splits, &split_len);
   f2* p = splits > 1 ? part : nullptr;
   hipLaunchKernelGGL(nbody_accel_kernel, dim3(blocks_for(nt, kBlock * kTargetsPerLane), splits),
-                     dim3(kBlock), 0, s, pos, ns_padded, t0, nt, eps2, gm, split_len, p, ax, ay);
+                     dim3(kBlock), 0, s, pos, ns_padded, t0, nt, eps2, gm, split_len, p, ax, ay, stamps);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !p) return e;
   hipLaunchKernelGGL(nbody_reduce_kernel, dim3(blocks_for(nt)), dim3(kBlock), 0, s, p, splits, nt, gm,

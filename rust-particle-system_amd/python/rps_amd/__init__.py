@@ -189,6 +189,7 @@ ABI_SYMBOLS = [
     ("rps_get_counters", _I, [_P, ctypes.POINTER(_U32), ctypes.POINTER(_U64)]),
     ("rps_set_profiling", _I, [_P, _I]),
     ("rps_get_kernel_time", _I, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64)]),
+    ("rps_get_kernel_clock", _I, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64)]),
     ("rps_time_steps", _I, [_P, _U32, ctypes.POINTER(ctypes.c_double)]),
     ("rps_get_stream", _P, [_P]),
     ("rps_step_cost", _I, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I)]),
@@ -524,6 +525,13 @@ class Context:
         ms, cnt = ctypes.c_double(), ctypes.c_uint64()
         self._call("rps_get_kernel_time", ctypes.byref(ms), ctypes.byref(cnt))
         return ms.value, cnt.value
+
+    def kernel_clock(self):
+        """(MHz, workgroups): the shader clock sustained by the last profiled N-body force
+        launch, the median over its workgroups (rps_get_kernel_clock)."""
+        mhz, cnt = ctypes.c_double(), ctypes.c_uint64()
+        self._call("rps_get_kernel_clock", ctypes.byref(mhz), ctypes.byref(cnt))
+        return mhz.value, cnt.value
 
     def time_steps(self, nsteps: int) -> float:
         ms = ctypes.c_double()

@@ -26,6 +26,12 @@ def copy_d2d(dst, src, nbytes):
     assert hip().hipMemcpy(ctypes.c_void_p(dst), ctypes.c_void_p(src), nbytes, 3) == 0
 
 
+def copy_h2d(dst, host: np.ndarray):
+    """hipMemcpy host -> device of a contiguous numpy array (dst: raw device pointer)."""
+    host = np.ascontiguousarray(host)
+    assert hip().hipMemcpy(ctypes.c_void_p(dst), host.ctypes.data_as(ctypes.c_void_p), host.nbytes, 1) == 0
+
+
 class DeviceBuffer:
     def __init__(self, nbytes):
         self.ptr = ctypes.c_void_p()

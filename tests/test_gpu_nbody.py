@@ -242,3 +242,57 @@ def test_nbody_full_size(gpu, orc, monkeypatch, n, splits):
     ref = copy_soa(soa)
     orc.nbody_integrate(cfg, ext, ax, ay, ref)
     assert_soa_bitwise(got, ref)
+
+
+@pytest.mark.parametrize("splits", [None, "3"])
+def test_nbody_c5_rank_shard(gpu, orc, monkeypatch, splits):
+    """BASELINE.json's C5 (2^27 particles all-pairs over 8 x MI355X) as one rank sees it, on
+    one GPU: rank 7's targets start at id_offset 7 * 2^24 and its sources are all 2^27 global
+    particles -- the 1-GiB float2 array its ncclAllGather would fill, filled here by the test
+    (RPS_EXT_NBODY_EXTERNAL + rps_nbody_sources, host -> device) -- so the source loop, the
+    64-bit source and target offsets and the splits run at C5's shape.  2^20 targets (the
+    full 2^24-target shard is ~6 min on one GPU; the kernel's work per target is the same):
+    the default split count for that launch, and 3 splits, what a full 2^24-target C5 shard
+    picks (8192 target blocks x 3 >= 24 576).  Four chunks of 16 targets against the f64
+    oracle over every one of the 2^27 sources (the bound of the other full-size tests);
+    integration bitwise."""
+    from hip_mem import copy_h2d
+
+    if splits:
+        monkeypatch.setenv("RPS_NBODY_SPLITS", splits)
+    rps = gpu
+    ng, n = 1 << 27, 1 << 20
+    off = 7 << 24
+    cfg = config_c1(rps, min(ng, 0xFFFFFFFF))
+    ext = rps.make_ext(nbody_strength=1.0e3, nbody_softening=1.0, shader_delay=0)
+    ext.flags |= rps.EXT_NBODY_EXTERNAL
+    g = np.random.default_rng(27)
+    pos = np.empty((ng, 2), F)
+    pos[:, 0] = g.uniform(-950, 950, ng).astype(F)
+    pos[:, 1] = g.uniform(-530, 530, ng).astype(F)
+    soa = dict(x=pos[off:off + n, 0].copy(), y=pos[off:off + n, 1].copy(),
+               vx=g.normal(0, 10, n).astype(F), vy=g.normal(0, 10, n).astype(F))
+    with rps.Context(n, rps.MODE_NBODY, id_offset=off, global_count=ng) as ctx:
+        ctx.set_config(cfg, ext)
+        ctx.upload_soa(soa)
+        src, cnt = ctx.nbody_sources(pack=True)
+        assert cnt == ng
+        copy_h2d(src, pos[:off])  # the other ranks' shards, as the all-gather would place them
+        copy_h2d(src + (off + n) * 8, pos[off + n:])
+        ctx.step(1)
+        ax = ctx.read_debug(rps.DEBUG_ACCEL_X)
+        ay = ctx.read_debug(rps.DEBUG_ACCEL_Y)
+        got = ctx.download_soa()
+    sx, sy = np.ascontiguousarray(pos[:, 0]), np.ascontiguousarray(pos[:, 1])
+    del pos
+    for rel in (0, 2048 * 8 + 5, n // 2 + 123, n - 16):
+        rx, ry, ab = orc.nbody_accel_ref(ext, sx, sy, t0=off + rel, nt=16)
+        gx, gy = ax[rel:rel + 16], ay[rel:rel + 16]
+        mag = np.hypot(rx.astype(np.float64), ry.astype(np.float64))
+        err = np.hypot(gx.astype(np.float64) - rx, gy.astype(np.float64) - ry)
+        bound = np.maximum(1e-4 * mag, 1e-5 * ab)
+        assert np.max(err / bound) <= 1.0, (rel, np.max(err / bound))
+        assert np.median(err / mag) < 1e-5, (rel, np.median(err / mag))
+    ref = copy_soa(soa)
+    orc.nbody_integrate(cfg, ext, ax, ay, ref)
+    assert_soa_bitwise(got, ref)

@@ -184,27 +184,38 @@ def test_sph_bench_workload_full_size(gpu, orc, n):
     _frames_vs_oracle(rps, orc, n, soa, cfg, 2)
 
 
-@pytest.mark.parametrize("n", [4096, 3000])
-def test_sph_frame_cost_counts(gpu, orc, n):
+@pytest.mark.parametrize("n,layout", [(4096, "0"), (3000, "0"), (4096, "2")])
+def test_sph_frame_cost_counts(gpu, orc, monkeypatch, n, layout):
     """rps_sph_frame_cost's device counts (the roofline's E) equal the entries of every lookup
     slot's nine runs, walked here on the oracle's lookup, offsets and predicted positions the
     way the reference's scans walk them (wgsl:231-252): keys in the reference cell order, a
-    run ends at a key change or at N.  The byte model follows include/rps.h."""
+    run ends at a key change or at N.  The byte model follows include/rps.h.  Layout "2": the
+    spatial record layout forced (the count walks its storage runs, run2, over storage-order
+    predictions).  The query is refused before any active frame and after a gated one."""
     import ref_numpy as RN
 
     rps = gpu
+    monkeypatch.setenv("RPS_SPH_LAYOUT", layout)
     cfg = rps.default_particle_config(n, gravity=100.0)
     soa = _blob(n, 40 + n)
     st = orc.SphState(n)
     ref = copy_soa(soa)
     with rps.Context(n, rps.MODE_SPH) as ctx:
-        ctx.set_config(cfg, rps.make_ext(shader_delay=0))
+        ctx.set_config(cfg, rps.make_ext(shader_delay=2))
         ctx.upload_soa(soa)
+        ctx.step(1)  # frame 1 < SHADER_DELAY 2: gated
         with pytest.raises(rps.RpsError):
             ctx.sph_frame_cost()  # no active frame yet
-        ctx.step(1)
+        ctx.step(1)  # frame 2: active
         cost = ctx.sph_frame_cost()
         amt, unit = ctx.step_cost()
+        ctx.set_config(cfg, rps.make_ext(shader_delay=2))  # frame_count back to 0
+        ctx.step(1)  # gated again: lookup re-sorted, predictions of the older frame
+        with pytest.raises(rps.RpsError):
+            ctx.sph_frame_cost()
+        with pytest.raises(rps.RpsError):
+            ctx.step_cost()
+    st.grid(cfg, ref)
     st.grid(cfg, ref)
     st.pre(cfg, ref)
     P = st.P
@@ -235,13 +246,13 @@ def test_sph_frame_cost_counts(gpu, orc, n):
     assert cost["frame_bytes"] == cost["sort_bytes"] + cost["predict_bytes"] + cost["density_bytes"] + cost["sim_bytes"]
 
 
-@pytest.mark.parametrize("case", ["blob", "dense", "outside", "xcd", "batches"])
+@pytest.mark.parametrize("case", ["blob", "dense", "outside", "batches"])
 def test_sph_spatial_layout_forced(gpu, orc, monkeypatch, case):
     """The spatial record layout (rps_kernels.hip; by default only from 2^21 particles) forced
     at small P == N, every pass bitwise: an ordinary blob; a dense one whose runs exceed the
     runs kernel's 32-entry measure (the listed-run path); particles far outside the walls
     (runs owned by cells beyond the grid, lanes whose 3 x 3 block leaves it) with a radius +
-    bounds change mid-run (a new grid); XCD-banded workgroups; other scan batches.  The
+    bounds change mid-run (a new grid); other scan batches.  The
     16 384-particle default viewport has ~28 700 cells, within the context's cell capacity
     (at least 2^16), so every frame here runs the layout."""
     rps = gpu
@@ -259,8 +270,6 @@ def test_sph_spatial_layout_forced(gpu, orc, monkeypatch, case):
         soa["x"][100:140] = np.float32(961.0)
         cfg_at = {2: rps.default_particle_config(n, gravity=100.0, smoothing_radius=14.0,
                                                  screen_bounds=rps.screen_bounds_for(2400.0, 1400.0))}
-    if case == "xcd":
-        monkeypatch.setenv("RPS_SPH_XCD", "1")
     if case == "batches":  # the layout's other scan variants (default: density 8, sim 4)
         monkeypatch.setenv("RPS_SPH_BATCH_S", "6")
         monkeypatch.setenv("RPS_SPH_BATCH_D", "16")
@@ -295,3 +304,50 @@ def test_sph_spatial_layout_gated_frames(gpu, orc, monkeypatch):
                 st.sim(cfg, ref)
             assert_bitwise(ctx.read_debug(rps.DEBUG_LOOKUP_OFFSETS), st.offsets, f"offsets f{frame}")
             assert_soa_bitwise(ctx.download_soa(), ref, what=f"f{frame} ")
+
+
+def test_sph_layout_clustered_runs(gpu, orc, monkeypatch):
+    """Runs longer than the layout's 32-entry measure (a clump of particles in one cell) are
+    'listed' by the runs kernel.  Their lengths come from the per-key run ends and their slots'
+    prediction is spread over every thread of the write kernel (round 2 walked and predicted
+    each listed run on one lane, O(run length) dependent loads).  At 2^21 (the layout's default
+    from there on) with 16 clumps of 4096 particles each inside one cell: the first frame
+    bitwise against the oracle, and the layout frame no slower than 1.5x the lookup-order
+    frame of the same state (same clumps, same scans; only the record placement differs)."""
+    rps = gpu
+    n = 1 << 21
+    scale = (n / 50000) ** 0.5
+    cfg = rps.default_particle_config(n, screen_bounds=rps.screen_bounds_for(1920.0 * scale, 1080.0 * scale))
+    parts = rps.setup_particles_scatter(cfg, n, seed=0x5EED)
+    soa = dict(x=parts["position"][:, 0].copy(), y=parts["position"][:, 1].copy(),
+               vx=parts["velocity"][:, 0].copy(), vy=parts["velocity"][:, 1].copy())
+    g = np.random.default_rng(77)
+    r = float(cfg.smoothing_radius)
+    b = list(cfg.screen_bounds)
+    k = 4096
+    for c in range(16):
+        cx = np.floor(g.uniform(b[0] + 4 * r, b[1] - 4 * r) / r) * r + 0.5 * r
+        cy = np.floor(g.uniform(b[2] + 4 * r, b[3] - 4 * r) / r) * r + 0.5 * r
+        sl = slice(c * k, (c + 1) * k)
+        soa["x"][sl] = (cx + g.uniform(-0.2 * r, 0.2 * r, k)).astype(F)
+        soa["y"][sl] = (cy + g.uniform(-0.2 * r, 0.2 * r, k)).astype(F)
+    ext = rps.make_ext(shader_delay=0)
+    ms = {}
+    for layout in ("1", "0"):
+        monkeypatch.setenv("RPS_SPH_LAYOUT", layout)
+        with rps.Context(n, rps.MODE_SPH) as ctx:
+            ctx.set_config(cfg, ext)
+            ctx.upload_soa(soa)
+            ctx.step(1)
+            if layout == "1":
+                st = orc.SphState(n, omp=True)
+                ref = copy_soa(soa)
+                st.grid(cfg, ref)
+                st.pre(cfg, ref)
+                assert_bitwise(ctx.read_debug(rps.DEBUG_DENSITIES), st.dens, "dens")
+                st.sim(cfg, ref)
+                assert_soa_bitwise(ctx.download_soa(), ref, what="clustered ")
+            ctx.upload_soa(soa)  # the same start state for both timings
+            ctx.step(2)
+            ms[layout] = ctx.time_steps(5) / 5
+    assert ms["1"] <= 1.5 * ms["0"], ms

@@ -208,3 +208,23 @@ def test_nbody_f32_baseline_port_close_to_oracle(rps, orc):
     tx, ty = orc.nbody_accel_f32_omp(ext, x, y, t0=500, nt=100, threads=2)
     assert_bitwise(tx, bx[500:600])
     assert_bitwise(ty, by[500:600])
+
+
+def test_nbody_reference_with_abs_sum(rps, orc):
+    """orc_nbody_accel_ref (the full-size N-body tests' checker, OpenMP over targets): the same
+    accelerations as orc_nbody_accel bit for bit at any thread count, and G * sum_j |f_ij|
+    equal to a numpy f64 direct sum."""
+    ext = rps.make_ext(nbody_strength=3.0, nbody_softening=0.7, shader_delay=0)
+    g = np.random.default_rng(12)
+    x = g.uniform(-200, 200, 1500).astype(F)
+    y = g.uniform(-100, 100, 1500).astype(F)
+    ax, ay = orc.nbody_accel(ext, x, y, t0=200, nt=300)
+    for threads in (1, 3):
+        rx, ry, ab = orc.nbody_accel_ref(ext, x, y, t0=200, nt=300, threads=threads)
+        assert_bitwise(rx, ax)
+        assert_bitwise(ry, ay)
+    dx = x[None, :].astype(np.float64) - x[200:500, None]
+    dy = y[None, :].astype(np.float64) - y[200:500, None]
+    d2 = dx * dx + dy * dy
+    ref = 3.0 * (np.sqrt(d2) * (d2 + F(0.7) * F(0.7)) ** -1.5).sum(1)
+    np.testing.assert_allclose(ab, ref, rtol=1e-12)
