@@ -22,6 +22,7 @@ Prints ONE JSON line on rank 0 (fields: see the contract in DESIGN.md §6).
 import argparse
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -31,6 +32,8 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 METRIC = "particle-updates/sec + achieved HBM GB/s, 10^8 particles, 1/2/4/8 MI355X"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector peak at the 2400-MHz max clock
+FP32_PEAK_CLOCK_MHZ = 2400.0
 L2_PEAK_GBPS = 34500.0  # MI355X_MICROARCH.md §L2: aggregate over the 8 XCDs, ~34.5 TB/s
 # SURVEY.md §8(d) / BASELINE.md, C3: the algorithmic cost of a particle-step is 40 B (read and
 # write x, y, vx, vy and an f32 lifetime).  The kernel moves 32.03 of them (the lifetime is a u16
@@ -52,8 +55,9 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=1 << 22, help="CPU-baseline particles")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=0x5EED)
-    ap.add_argument("--profile-every", type=int, default=8,
-                    help="bracket every k-th kernel launch with HIP events (roofline.achieved)")
+    ap.add_argument("--profile-every", type=int, default=0,
+                    help="bracket every k-th kernel launch with HIP events (roofline.achieved); 0: every "
+                         "launch up to 64 timed steps, every (steps // 64)-th beyond; -1: off")
     ap.add_argument("--allpairs-n", type=int, default=1 << 22,
                     help="global particles of the all-pairs N-body side measurement (0: skip)")
     ap.add_argument("--allpairs-steps", type=int, default=2)
@@ -245,15 +249,27 @@ def allpairs(rps, args, d):
         el = d.max(t1 - t0)
         kms, _ = ctx.kernel_time()
         kms = d.max(kms)
+        # The shader clock the chip held under the force kernel (median over its workgroups of
+        # in-kernel s_memtime / s_memrealtime stamps, last timed launch; rps_get_kernel_clock).
+        clk_mhz, clk_wgs = ctx.kernel_clock()
+        clk_mhz = -d.max(-clk_mhz)  # the slowest rank's clock
     finally:
         ctx.close()
     inter = float(ng) * ng * args.allpairs_steps
     flop = 20.0 * float(n) * ng  # per rank per step (GPU Gems 3 convention, rsqrt = 4)
+    tf = flop / (kms * 1e-3) / 1e12
+    peak_at_clk = FP32_PEAK_TFLOPS * clk_mhz / FP32_PEAK_CLOCK_MHZ
     return {"workload": f"all-pairs softened gravity, {ng} global particles, index-sharded x{d.world}",
             "scaling": "strong", "steps": args.allpairs_steps, "ms_per_step": el * 1e3 / args.allpairs_steps,
             "interactions_per_s": inter / el, "force_kernel_ms": kms,
-            "roofline": {"bound": "valu", "achieved": flop / (kms * 1e-3) / 1e12, "peak": 157.3,
-                         "unit": "TFLOP/s", "frac": flop / (kms * 1e-3) / 1e12 / 157.3},
+            "roofline": {"bound": "valu", "achieved": tf, "peak": FP32_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": tf / FP32_PEAK_TFLOPS,
+                         "sustained_clock_mhz": clk_mhz, "clock_samples": clk_wgs,
+                         "peak_at_sustained_clock": peak_at_clk, "frac_at_sustained_clock": tf / peak_at_clk,
+                         "issue_floor_frac": 0.822,
+                         "note": "peak 157.3 TF assumes 2400 MHz; frac_at_sustained_clock divides by the peak "
+                                 "at the clock the chip held (in-kernel stamps), i.e. the clock-independent share; "
+                                 "the loop's issue floor is 0.822 of either (DESIGN.md §5)"},
             "collective": f"ncclAllGather {8 * ng} B per step" if d.dist else "none (no launcher)",
             **({"cpu_baseline": allpairs_cpu_baseline(rps, args, ext)}
                if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline and args.allpairs_cpu_n > 0 else {})}
@@ -480,7 +496,8 @@ def main():
 
     d.sync_device()
     d.barrier()
-    ctx.set_profiling(args.profile_every)
+    period = args.profile_every if args.profile_every else max(1, args.steps // 64)
+    ctx.set_profiling(max(0, period))
     t0 = time.perf_counter()
     ctx.step(args.steps)
     ctx.sync()
@@ -488,8 +505,14 @@ def main():
     t1 = time.perf_counter()
     d.barrier()
     elapsed = d.max(t1 - t0)
-    kern_ms, launches = ctx.kernel_time()
-    kern_ms = d.max(kern_ms)
+    # Per-launch durations of the bracketed launches (HIP events on the context stream); the
+    # roofline uses their median, so a launch with a late event or a slow first dispatch does
+    # not set it.
+    times = ctx.kernel_times() if period > 0 else []
+    launches = len(times)
+    kern_med = d.max(statistics.median(times)) if times else float("nan")
+    kern_mean = d.max(statistics.mean(times)) if times else float("nan")
+    kern_ms = kern_med
     moved_per_launch, _ = ctx.step_cost()  # bytes the kernel moves: 32.03 B per particle
     algo_per_launch = ALGO_BYTES_PER_PARTICLE * n
     export = export_side(ctx, n, args.export_reps) if args.export_reps > 0 and hasattr(ctx, "stream_ptr") else None
@@ -525,7 +548,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS,
                      "traffic": traffic, "kernel": "stream_step_kernel<euler,lifetime>",
-                     "avg_kernel_ms": kern_ms, "launches": launches,
+                     "median_kernel_ms": kern_med, "avg_kernel_ms": kern_mean, "launches": launches,
+                     "profile_every": period,
                      "algorithmic_bytes_per_launch": algo_per_launch,
                      "moved_bytes_per_launch": moved_per_launch, "moved_gbps": moved_gbps,
                      "moved_frac": moved_gbps / HBM_PEAK_GBPS,

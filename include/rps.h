@@ -259,6 +259,10 @@ int rps_set_profiling(rps_ctx* ctx, int period);
 /* Average duration (ms) and count of the bracketed dominant-kernel launches since profiling
  * was enabled; blocks until they completed. */
 int rps_get_kernel_time(rps_ctx* ctx, double* avg_ms, uint64_t* launches);
+/* The same launches one by one: the durations (ms, launch order) of up to `cap` of the
+ * bracketed launches since profiling was enabled, and their total count; blocks until they
+ * completed, and starts a new collection like rps_get_kernel_time. */
+int rps_get_kernel_times(rps_ctx* ctx, double* ms, uint64_t cap, uint64_t* launches);
 /* N-body: the shader clock the chip sustained during the most recent profiled force launch
  * (median over its workgroups of delta s_memtime / delta s_memrealtime x 100 MHz, stamped at
  * each workgroup's start and end), in MHz, and the number of workgroups it is the median of.

@@ -1070,6 +1070,21 @@ int rps_get_kernel_time(rps_ctx* ctx, double* avg_ms, uint64_t* launches) {
   return RPS_OK;
 }
 
+int rps_get_kernel_times(rps_ctx* ctx, double* ms, uint64_t cap, uint64_t* launches) {
+  int rc = check_ctx(ctx);
+  if (rc) return rc;
+  if (!ms && cap) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "null output");
+  RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  for (size_t i = 0; i < ctx->ev_used && i < cap; ++i) {
+    float t = 0.0f;
+    RPS_HIP(ctx, hipEventElapsedTime(&t, ctx->ev_start[i], ctx->ev_stop[i]));
+    ms[i] = t;
+  }
+  if (launches) *launches = ctx->ev_used;
+  ctx->ev_used = 0;
+  return RPS_OK;
+}
+
 int rps_time_steps(rps_ctx* ctx, uint32_t nsteps, double* total_ms) {
   int rc = check_ctx(ctx);
   if (rc) return rc;

@@ -848,6 +848,118 @@ __global__ __launch_bounds__(1024) void sph_sort_local_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Static-network tail launch.  After a later stage's global passes (strides >= the tile), what
+// is left of the stage inside each tile is always the same network: the TLOG non-flip passes
+// of strides 2^(TLOG-1), ..., 2, 1.  With the strides known at compile time every LDS address
+// is one per-thread base plus an immediate offset (PaddedTile's pad folds into it: padded(e0 +
+// j*g) = padded(e0) + j*g + (j*g >> 5) for a group's base aligned to 2G and residue r < g), and
+// the first and last register chunks talk to memory directly: the first loads its eight
+// entries (strides 2^(TLOG-1..TLOG-3), group r = thread) from the lookup, the last (strides 8,
+// 4, 2, 1) is a 16-entry group held by a lane pair, eight consecutive entries per lane, whose
+// stride-8 pass exchanges entries across the pair with a DPP move, and stores them.  Two LDS
+// sweeps fewer than staging the tile (round 2: load sweep, five chunk sweeps, store sweep).
+// Same compare-swaps in the same pass order as the reference's dispatch sequence.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void cas(uint2& lo, uint2& hi) {
+  if (lo.x > hi.x) {
+    const uint2 t = lo;
+    lo = hi;
+    hi = t;
+  }
+}
+
+// The non-flip passes of strides g*2^(K-1), ..., g over the 2^K entries v[j] = position
+// r + j*g of one group (sort_group's inner loop with M = 2^K).
+template <int K>
+__device__ __forceinline__ void group_passes(uint2 (&v)[1 << K]) {
+#pragma unroll
+  for (int m = K - 1; m >= 0; --m)
+#pragma unroll
+    for (int j = 0; j < (1 << K); ++j)
+      if (!(j & (1 << m))) cas(v[j], v[j + (1 << m)]);
+}
+
+// Padded LDS index offset of the group's entry j (see above).
+template <uint32_t G>
+__device__ __forceinline__ constexpr uint32_t pad_off(uint32_t j) {
+  return j * G + ((j * G) >> 5);
+}
+__device__ __forceinline__ uint32_t padded(uint32_t e) { return e + (e >> 5); }
+
+// One LDS chunk: passes of strides 2^LG down to 2^(LG-K+1), non-flip, 2^(3-K) groups per thread
+// (eight entries), thread t taking groups t * 2^(3-K) + i.
+template <int LG, int K>
+__device__ __forceinline__ void lds_chunk(uint2* lds, uint32_t t) {
+  constexpr int LGG = LG - K + 1;
+  constexpr uint32_t g = 1u << LGG;
+  constexpr int NG = 1 << (3 - K);
+#pragma unroll
+  for (int i = 0; i < NG; ++i) {
+    const uint32_t q = t * NG + i;
+    const uint32_t e0 = ((q >> LGG) << (LG + 1)) + (q & (g - 1u));
+    const uint32_t a = padded(e0);
+    uint2 v[1 << K];
+#pragma unroll
+    for (int j = 0; j < (1 << K); ++j) v[j] = lds[a + pad_off<g>(j)];
+    group_passes<K>(v);
+#pragma unroll
+    for (int j = 0; j < (1 << K); ++j) lds[a + pad_off<g>(j)] = v[j];
+  }
+}
+
+// The middle chunks: strides 2^LG down to 2^4, three passes per chunk (the last one fewer);
+// a chunk whose span 2G exceeds one wave's 512 entries ends with a workgroup barrier.
+template <int LG>
+__device__ __forceinline__ void lds_chunks(uint2* lds, uint32_t t) {
+  if constexpr (LG >= 4) {
+    constexpr int K = LG - 3 >= 3 ? 3 : LG - 3;
+    lds_chunk<LG, K>(lds, t);
+    if constexpr ((2 << LG) > 512) __syncthreads();
+    else wave_lds_sync();
+    lds_chunks<LG - K>(lds, t);
+  }
+}
+
+template <int TLOG>
+__global__ __launch_bounds__(1u << (TLOG - 3)) void sph_sort_tail_kernel(uint2* __restrict__ lookup) {
+  static_assert(TLOG >= 10 && TLOG <= 13, "eight entries per thread, 128..1024 threads");
+  constexpr uint32_t TILE = 1u << TLOG, NT = TILE / 8;
+  __shared__ uint2 lds[TILE + TILE / 32];
+  const uint32_t t = threadIdx.x;
+  uint2* tile = lookup + (size_t)blockIdx.x * TILE;
+  {  // strides TILE/2, TILE/4, TILE/8: group r = t, entries t + j * NT, straight from the lookup
+    uint2 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = tile[t + j * NT];
+    group_passes<3>(v);
+    const uint32_t a = padded(t);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) lds[a + pad_off<NT>(j)] = v[j];
+  }
+  __syncthreads();
+  lds_chunks<TLOG - 4>(lds, t);
+  {  // strides 8, 4, 2, 1: lane pair (2k, 2k + 1) holds the 16 entries [16k, 16k + 16)
+    const uint32_t a = padded(8u * t);
+    uint2 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = lds[a + i];
+    const bool left = (t & 1u) == 0u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {  // stride 8: entry i of the left lane against entry i of the right
+      uint2 p;
+      p.x = (uint32_t)__builtin_amdgcn_mov_dpp((int)v[i].x, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
+      p.y = (uint32_t)__builtin_amdgcn_mov_dpp((int)v[i].y, 0xB1, 0xF, 0xF, false);
+      const bool swap = left ? (v[i].x > p.x) : (p.x > v[i].x);
+      v[i] = swap ? p : v[i];
+    }
+    group_passes<3>(v);  // strides 4, 2, 1 inside the lane's eight
+    uint4* out = reinterpret_cast<uint4*>(tile + 8u * t);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[i] = make_uint4(v[2 * i].x, v[2 * i].y, v[2 * i + 1].x, v[2 * i + 1].y);
+  }
+}
+
 // All T global passes of one stage in one launch (T > 4 would take two or more register-fused
 // launches).  The passes have strides G = 2^s down to g = 2^lg (the LDS tile of the local
 // launches); as in sort_group, residue class r (positions r + j*g of a 2G block, j < 2^T)
@@ -1103,6 +1215,50 @@ __device__ __forceinline__ uint32_t nine_runs(const RunBounds& rb, float px, flo
   return c;
 }
 
+// The nine runs as pairs of storage-adjacent entries: each merged run of len entries is
+// ceil(len / 2) pairs, pair k of a run holding its entries 2k and 2k + 1 (the last pair of an
+// odd run only 2k), so one 16-B load fetches two neighbours.  Table entry per run: {slot of its
+// first entry - 2 * its first pair index, its pair end | its flat-entry end << 16}; a pair p
+// of that run starts at slot 2p + x and flat index 2p - d, d = 2 * (pair end) - (flat end)
+// of the run before (the odd runs so far).  Returns the pair count; *total_out the entries.
+// Only for totals below 2^16 entries (callers fall back to nine_runs beyond).
+template <bool LAYOUT>
+__device__ __forceinline__ uint32_t nine_runs_pairs(const RunBounds& rb, float px, float py, float xoff,
+                                                    float yoff, float r, uint32_t N, RunTable& runs,
+                                                    uint32_t* total_out) {
+  const uint32_t total = nine_runs<LAYOUT>(rb, px, py, xoff, yoff, r, N, runs);
+  *total_out = total;
+  if (total >= 65536u) return 0;
+  uint32_t pairs = 0, fend = 0;
+  for (uint32_t k = 0; fend < total; ++k) {  // rewrite the entry table in place
+    const uint2 e = runs[k][threadIdx.x];  // {slot - flat start, flat end}
+    const uint32_t f0 = fend;
+    fend = e.y;
+    const uint32_t p0 = pairs;
+    pairs += (fend - f0 + 1u) >> 1;
+    runs[k][threadIdx.x] = make_uint2(e.x + f0 - 2u * p0, pairs | (fend << 16));
+  }
+  return pairs;
+}
+
+struct PairCursor {
+  const RunTable& runs;
+  uint32_t r = 0, d = 0;
+  uint2 cur;
+  __device__ explicit PairCursor(const RunTable& t) : runs(t), cur(t[0][threadIdx.x]) {}
+  // Pair p (non-decreasing p < pairs): its first entry's slot and flat index, and whether its
+  // second entry exists.
+  __device__ __forceinline__ uint32_t slot(uint32_t p, uint32_t& f, bool& second) {
+    if (p >= (cur.y & 0xFFFFu)) {  // runs are non-empty: one step suffices
+      d = 2u * (cur.y & 0xFFFFu) - (cur.y >> 16);
+      cur = runs[++r][threadIdx.x];
+    }
+    f = 2u * p - d;
+    second = f + 1u < (cur.y >> 16);
+    return 2u * p + cur.x;
+  }
+};
+
 // Walks the flat index forward: slot(f) for non-decreasing f < total.
 struct RunCursor {
   const RunTable& runs;
@@ -1138,7 +1294,10 @@ struct RunCursor {
 //
 // calculate_density, compute_shader.wgsl:207-254: entries summed in run order, kScanBatch
 // predicted positions in flight per lane across run boundaries.
-template <int kScanBatch, bool LAYOUT>
+// PAIRS: the scan walks pairs of storage-adjacent entries (nine_runs_pairs), one 16-B load per
+// pair instead of one 8-B load per entry -- half the load instructions, and with them the
+// texture-address work that bounds this scan; the same entries in the same order.
+template <int kScanBatch, bool LAYOUT, bool PAIRS>
 __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* __restrict__ cfg,
                                                              RunBounds rb, SphSlots sl, uint32_t p_slots) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
@@ -1148,42 +1307,72 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
   const uint32_t N = cfg->particle_count;
   const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
   __shared__ RunTable runs;
-  const uint32_t total = nine_runs<LAYOUT>(rb, p[0], p[1], cfg->screen_bounds[1],
-                                   cfg->screen_bounds[3], r, N, runs);
-  RunCursor rc(runs);
   float d = 0.0f, nd = 0.0f;
   uint64_t m0 = 0, m1 = 0;
-  for (uint32_t f = 0; f < total; f += kScanBatch) {
-    f2 q[kScanBatch];
+  uint32_t total;
+  // One neighbour entry at flat index b (calculate_density's loop body, wgsl:238-252).
+  const auto entry = [&](f2 q, uint32_t b) {
+    const float dx = p[0] - q[0], dy = p[1] - q[1];
+    const float sq = dx * dx + dy * dy;
+    if (!(sq > r2)) {
+      if (total <= 128u) {  // otherwise the sim pass scans the runs (masks unused)
+        if (b < 64u) m0 |= 1ull << b;
+        else m1 |= 1ull << (b - 64u);
+      }
+      // Correctly rounded sqrt without the input scaling unless a lane of the wave needs it
+      // (0 < sq < 2^-96: two particles closer than ~1e-14, only ever near the origin):
+      // the same bits as sqrtf (tools/sqrt_check.hip, every input), 2^22 frame
+      // 1.2461 -> 1.2358 ms (same box).
+      const bool tiny = sq > 0.0f && sq < 0x1p-96f;
+      const float dist = __builtin_amdgcn_ballot_w64(tiny) ? sqrtf(sq) : sqrt_rn_unscaled(sq);
+      float k1 = 0.0f, k2 = 0.0f;
+      if (!(dist >= r)) {
+        const float v = r - dist;
+        k1 = (dn * v) * v;
+        k2 = ((ndn * v) * v) * v;
+      }
+      d = d + k1;
+      nd = nd + k2;
+    }
+  };
+  uint32_t pairs = 0;
+  if constexpr (PAIRS)
+    pairs = nine_runs_pairs<LAYOUT>(rb, p[0], p[1], cfg->screen_bounds[1], cfg->screen_bounds[3], r, N, runs,
+                                    &total);
+  else
+    total = nine_runs<LAYOUT>(rb, p[0], p[1], cfg->screen_bounds[1], cfg->screen_bounds[3], r, N, runs);
+  if (PAIRS && total < 65536u) {
+    // kScanBatch / 2 pairs in flight.  A pair's 16-B load may read the 8 B after the last slot
+    // (pp_s is followed by rec_pv in the arena); that half is never used.
+    constexpr int B = kScanBatch / 2;
+    PairCursor pc(runs);
+    for (uint32_t k = 0; k < pairs; k += B) {
+      f4 q[B];
+      uint32_t fb[B];
+      bool two[B];
 #pragma unroll
-    for (int u = 0; u < kScanBatch; ++u) q[u] = sl.pp_s[rc.slot(min(f + u, total - 1u))];
+      for (int u = 0; u < B; ++u) {
+        const uint32_t j = pc.slot(min(k + u, pairs - 1u), fb[u], two[u]);
+        typedef float f4a8 __attribute__((ext_vector_type(4), aligned(8)));
+        q[u] = *reinterpret_cast<const f4a8*>(sl.pp_s + j);
+      }
 #pragma unroll
-    for (int u = 0; u < kScanBatch; ++u) {
-      if (f + u < total) {
-        const float dx = p[0] - q[u][0], dy = p[1] - q[u][1];
-        const float sq = dx * dx + dy * dy;
-        if (!(sq > r2)) {
-          const uint32_t b = f + u;
-          if (total <= 128u) {  // otherwise the sim pass scans the runs (masks unused)
-            if (b < 64u) m0 |= 1ull << b;
-            else m1 |= 1ull << (b - 64u);
-          }
-          // Correctly rounded sqrt without the input scaling unless a lane of the wave needs it
-          // (0 < sq < 2^-96: two particles closer than ~1e-14, only ever near the origin):
-          // the same bits as sqrtf (tools/sqrt_check.hip, every input), 2^22 frame
-          // 1.2461 -> 1.2358 ms (same box).
-          const bool tiny = sq > 0.0f && sq < 0x1p-96f;
-          const float dist = __builtin_amdgcn_ballot_w64(tiny) ? sqrtf(sq) : sqrt_rn_unscaled(sq);
-          float k1 = 0.0f, k2 = 0.0f;
-          if (!(dist >= r)) {
-            const float v = r - dist;
-            k1 = (dn * v) * v;
-            k2 = ((ndn * v) * v) * v;
-          }
-          d = d + k1;
-          nd = nd + k2;
+      for (int u = 0; u < B; ++u) {
+        if (k + u < pairs) {
+          entry(f2{q[u][0], q[u][1]}, fb[u]);
+          if (two[u]) entry(f2{q[u][2], q[u][3]}, fb[u] + 1u);
         }
       }
+    }
+  } else {
+    RunCursor rc(runs);
+    for (uint32_t f = 0; f < total; f += kScanBatch) {
+      f2 q[kScanBatch];
+#pragma unroll
+      for (int u = 0; u < kScanBatch; ++u) q[u] = sl.pp_s[rc.slot(min(f + u, total - 1u))];
+#pragma unroll
+      for (int u = 0; u < kScanBatch; ++u)
+        if (f + u < total) entry(q[u], f + u);
     }
   }
   sl.nbr_mask[t] = m0;
@@ -1932,8 +2121,16 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
       if (e != hipSuccess) return e;
       step += k;
     }
-    if (step <= stage) {
-      e = launch_sort_local(kmax, false, tiles, lt, s, b.lookup, tile, stage, stage, step, nobin);
+    if (step <= stage) {  // the stage's passes inside each tile: strides tile/2 .. 1
+      switch (tile_log) {
+        case 13: hipLaunchKernelGGL((sph_sort_tail_kernel<13>), dim3(tiles), dim3(1024), 0, s, b.lookup); break;
+        case 12: hipLaunchKernelGGL((sph_sort_tail_kernel<12>), dim3(tiles), dim3(512), 0, s, b.lookup); break;
+        case 11: hipLaunchKernelGGL((sph_sort_tail_kernel<11>), dim3(tiles), dim3(256), 0, s, b.lookup); break;
+        default:
+          e = launch_sort_local(kmax, false, tiles, lt, s, b.lookup, tile, stage, stage, step, nobin);
+          if (e != hipSuccess) return e;
+      }
+      e = hipGetLastError();
       ++*launches;
       if (e != hipSuccess) return e;
     }
@@ -1971,10 +2168,10 @@ static hipError_t launch_sph_density(const SphBuffers& b, hipStream_t s) {
   const RunBounds rb = run_bounds(b);
 #define RPS_DENSITY(B)                                                                            \
   if (b.layout)                                                                                   \
-    hipLaunchKernelGGL((sph_density_kernel<B, true>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s, \
+    hipLaunchKernelGGL((sph_density_kernel<B, true, true>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s, \
                        b.cfg, rb, b.sl, b.p);                                               \
   else                                                                                            \
-    hipLaunchKernelGGL((sph_density_kernel<B, false>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s, \
+    hipLaunchKernelGGL((sph_density_kernel<B, false, true>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s, \
                        b.cfg, rb, b.sl, b.p)
   switch (sph_batch(true, b.p, b.batch_d, b.layout)) {
     case 4: RPS_DENSITY(4); break;

@@ -189,6 +189,7 @@ ABI_SYMBOLS = [
     ("rps_get_counters", _I, [_P, ctypes.POINTER(_U32), ctypes.POINTER(_U64)]),
     ("rps_set_profiling", _I, [_P, _I]),
     ("rps_get_kernel_time", _I, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64)]),
+    ("rps_get_kernel_times", _I, [_P, ctypes.POINTER(ctypes.c_double), _U64, ctypes.POINTER(_U64)]),
     ("rps_get_kernel_clock", _I, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64)]),
     ("rps_time_steps", _I, [_P, _U32, ctypes.POINTER(ctypes.c_double)]),
     ("rps_get_stream", _P, [_P]),
@@ -525,6 +526,14 @@ class Context:
         ms, cnt = ctypes.c_double(), ctypes.c_uint64()
         self._call("rps_get_kernel_time", ctypes.byref(ms), ctypes.byref(cnt))
         return ms.value, cnt.value
+
+    def kernel_times(self, cap: int = 1 << 16):
+        """Durations (ms, launch order) of the bracketed dominant-kernel launches since
+        profiling was enabled (rps_get_kernel_times); starts a new collection."""
+        buf = (ctypes.c_double * cap)()
+        cnt = ctypes.c_uint64()
+        self._call("rps_get_kernel_times", buf, cap, ctypes.byref(cnt))
+        return [buf[i] for i in range(min(cap, cnt.value))]
 
     def kernel_clock(self):
         """(MHz, workgroups): the shader clock sustained by the last profiled N-body force
