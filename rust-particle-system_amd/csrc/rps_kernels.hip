@@ -922,7 +922,7 @@ __device__ __forceinline__ void lds_chunks(uint2* lds, uint32_t t) {
 }
 
 template <int TLOG>
-__global__ __launch_bounds__(1u << (TLOG - 3)) void sph_sort_tail_kernel(uint2* __restrict__ lookup) {
+__global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_eu(4))) void sph_sort_tail_kernel(uint2* __restrict__ lookup) {
   static_assert(TLOG >= 10 && TLOG <= 13, "eight entries per thread, 128..1024 threads");
   constexpr uint32_t TILE = 1u << TLOG, NT = TILE / 8;
   __shared__ uint2 lds[TILE + TILE / 32];
@@ -958,6 +958,191 @@ __global__ __launch_bounds__(1u << (TLOG - 3)) void sph_sort_tail_kernel(uint2* 
 #pragma unroll
     for (int i = 0; i < 4; ++i) out[i] = make_uint4(v[2 * i].x, v[2 * i].y, v[2 * i + 1].x, v[2 * i + 1].y);
   }
+}
+
+// ---------------------------------------------------------------------------------------
+// Static-network head launch: bin (wgsl:455-468) + every stage whose whole network fits one
+// tile (stages 0 .. TLOG-1), eight entries per thread.  Between stages a thread holds its eight
+// consecutive entries [8t, 8t + 8) in registers, and lane quads the 32 entries [32k, 32k + 32):
+// passes of stride 1, 2, 4 run inside a lane, strides 8 and 16 (and the flips of stages 3
+// and 4) across the quad with DPP moves, so stages 0-4 and the last five passes of every later
+// stage never touch LDS.  A later stage S writes its entries to LDS once, runs its flip chunk
+// (strides 2^S, 2^(S-1)) and its passes of strides 2^(S-2) .. 32 there in register chunks with
+// compile-time addresses, and reads its entries back.  The last stage stores them.  Same
+// compare-swaps in the same order as the reference's pass-per-dispatch schedule.
+// ---------------------------------------------------------------------------------------
+
+// A pass across lanes: entry j of this lane against entry j (REV: 7 - j) of the DPP partner
+// (quad_perm CTRL); `left` = this lane holds the lower position of each pair.
+template <int CTRL, bool REV>
+__device__ __forceinline__ void xlane_pass(uint2 (&v)[8], bool left) {
+  uint2 p[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    p[j].x = (uint32_t)__builtin_amdgcn_mov_dpp((int)v[REV ? 7 - j : j].x, CTRL, 0xF, 0xF, false);
+    p[j].y = (uint32_t)__builtin_amdgcn_mov_dpp((int)v[REV ? 7 - j : j].y, CTRL, 0xF, 0xF, false);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const bool swap = left ? (v[j].x > p[j].x) : (p[j].x > v[j].x);
+    v[j] = swap ? p[j] : v[j];
+  }
+}
+constexpr int kDppXor1 = 0xB1;  // quad_perm [1, 0, 3, 2]
+constexpr int kDppXor2 = 0x4E;  // quad_perm [2, 3, 0, 1]
+constexpr int kDppRev4 = 0x1B;  // quad_perm [3, 2, 1, 0]
+
+// Stages 0-2 (spans 2, 4, 8): inside the lane's eight consecutive entries.
+__device__ __forceinline__ void reg_stages012(uint2 (&v)[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; i += 2) cas(v[i], v[i + 1]);  // stage 0: flip G = 1
+#pragma unroll
+  for (int b = 0; b < 8; b += 4) {  // stage 1: flip G = 2, then G = 1
+    cas(v[b], v[b + 3]);
+    cas(v[b + 1], v[b + 2]);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i += 2) cas(v[i], v[i + 1]);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) cas(v[j], v[7 - j]);  // stage 2: flip G = 4, then G = 2, 1
+#pragma unroll
+  for (int b = 0; b < 8; b += 4) {
+    cas(v[b], v[b + 2]);
+    cas(v[b + 1], v[b + 3]);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i += 2) cas(v[i], v[i + 1]);
+}
+
+// The flip chunk of stage S >= 5 in LDS: the flip pass (G = 2^S) and stride 2^(S-1), on the
+// residue class r and its mirror g - 1 - r (g = 2^(S-1), four entries each), thread t = group t.
+template <int S>
+__device__ __forceinline__ void lds_flip_chunk(uint2* lds, uint32_t t) {
+  constexpr uint32_t g = 1u << (S - 1);
+  constexpr int LP = S - 2;  // log2(groups per 2G block)
+  const uint32_t base = (t >> LP) << (S + 1), r = t & ((1u << LP) - 1u);
+  const uint32_t a = padded(base + r), b = padded(base + g - 1u - r);
+  uint2 v[8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[j] = lds[a + pad_off<g>(j)];
+    v[4 + j] = lds[b + pad_off<g>(j)];
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {  // flip: position r + j*g pairs with (g-1-r) + (3-j)*g
+    cas(v[j], v[7 - j]);
+    cas(v[4 + j], v[3 - j]);
+  }
+#pragma unroll
+  for (int c = 0; c < 8; c += 4) {  // stride g inside each class
+    cas(v[c], v[c + 1]);
+    cas(v[c + 2], v[c + 3]);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    lds[a + pad_off<g>(j)] = v[j];
+    lds[b + pad_off<g>(j)] = v[4 + j];
+  }
+}
+
+template <int SPAN>
+__device__ __forceinline__ void lds_sync() {
+  if constexpr (SPAN > 512) __syncthreads();
+  else wave_lds_sync();
+}
+
+// Non-flip strides 2^LG down to 32, register chunks of up to three passes; each chunk is
+// followed by the sync its span needs (the register tail reads the lane's own entries next).
+template <int LG>
+__device__ __forceinline__ void lds_mid_chunks(uint2* lds, uint32_t t) {
+  if constexpr (LG >= 5) {
+    constexpr int K = LG - 4 >= 3 ? 3 : LG - 4;
+    lds_chunk<LG, K>(lds, t);
+    lds_sync<(2 << LG)>();
+    lds_mid_chunks<LG - K>(lds, t);
+  }
+}
+
+// The register tail of a stage: strides 16 (if HI16), 8, 4, 2, 1.
+template <bool HI16>
+__device__ __forceinline__ void reg_tail(uint2 (&v)[8], uint32_t t) {
+  if constexpr (HI16) xlane_pass<kDppXor2, false>(v, (t & 2u) == 0u);
+  xlane_pass<kDppXor1, false>(v, (t & 1u) == 0u);
+  group_passes<3>(v);
+}
+
+template <int S, int TLOG>
+__device__ __forceinline__ void head_stages(uint2* lds, uint32_t t, uint2 (&v)[8]) {
+  if constexpr (S < TLOG) {
+    const uint32_t a = padded(8u * t);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) lds[a + i] = v[i];
+    lds_sync<(2 << S)>();
+    lds_flip_chunk<S>(lds, t);
+    lds_sync<(2 << S)>();
+    lds_mid_chunks<S - 2>(lds, t);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = lds[a + i];
+    reg_tail<(S >= 6)>(v, t);
+    // The next stage's first LDS write goes to this lane's own entries, which only this
+    // wave's chunks read in this stage once the last cross-wave chunk's barrier has passed.
+    head_stages<S + 1, TLOG>(lds, t, v);
+  }
+}
+
+template <int TLOG>
+__global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_eu(4))) void sph_sort_head_kernel(uint2* __restrict__ lookup, SortBin bin) {
+  static_assert(TLOG >= 10 && TLOG <= 13, "eight entries per thread, 128..1024 threads");
+  constexpr uint32_t TILE = 1u << TLOG, NT = TILE / 8;
+  __shared__ uint2 lds[TILE + TILE / 32];
+  const PaddedTile s{lds};
+  const uint32_t t = threadIdx.x;
+  const uint32_t base0 = blockIdx.x * TILE;
+  {  // bin: entry pairs q = 2t + 2k*NT, every position (or pad entry) load first, then the keys
+    f2 pa[4], pc[4];
+    uint4 lk[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      const uint32_t gq = base0 + 2u * t + k * 2u * NT;
+      if (gq < bin.n) {
+        pa[k] = bin_pos(bin, gq);
+        if (gq + 1u < bin.n) pc[k] = bin_pos(bin, gq + 1u);
+        else lk[k] = *reinterpret_cast<const uint4*>(lookup + gq);
+      } else {
+        lk[k] = *reinterpret_cast<const uint4*>(lookup + gq);
+      }
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      const uint32_t q = 2u * t + k * 2u * NT, gq = base0 + q;
+      uint2 a, c;
+      if (gq < bin.n) {
+        a = bin_key(bin, pa[k], gq);
+        c = gq + 1u < bin.n ? bin_key(bin, pc[k], gq + 1u) : make_uint2(lk[k].z, lk[k].w);
+      } else {
+        a = make_uint2(lk[k].x, lk[k].y);
+        c = make_uint2(lk[k].z, lk[k].w);
+      }
+      s[q] = a;
+      s[q + 1u] = c;
+    }
+  }
+  __syncthreads();
+  uint2 v[8];
+  const uint32_t a = padded(8u * t);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = lds[a + i];
+  reg_stages012(v);
+  xlane_pass<kDppXor1, true>(v, (t & 1u) == 0u);  // stage 3: flip G = 8 (lane pair), then 4, 2, 1
+  group_passes<3>(v);
+  xlane_pass<kDppRev4, true>(v, (t & 2u) == 0u);  // stage 4: flip G = 16 (lane quad), then 8 ... 1
+  reg_tail<false>(v, t);
+  // The bin's LDS image was read back by this lane only ([8t, 8t + 8)); its other entries were
+  // written by other waves before the barrier above, so stage 5's first write is safe.
+  head_stages<5, TLOG>(lds, t, v);
+  uint4* out = reinterpret_cast<uint4*>(lookup + base0 + 8u * t);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) out[i] = make_uint4(v[2 * i].x, v[2 * i].y, v[2 * i + 1].x, v[2 * i + 1].y);
 }
 
 // All T global passes of one stage in one launch (T > 4 would take two or more register-fused
@@ -2070,8 +2255,16 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
   // Stages whose whole network fits one tile: one launch (with the bin pass).
   const uint32_t first_global_stage = tile_log;  // stage s has 2*2^s = 2^(s+1) span
   const uint32_t lt = std::max(64u, std::min(1024u, tile >> kmax));
-  hipError_t e = launch_sort_local(kmax, true, tiles, lt, s, b.lookup, tile, 0u, first_global_stage - 1u,
-                                   0u, bin);
+  hipError_t e = hipSuccess;
+  switch (tile_log) {  // bin + stages [0, tile_log): the static-network head launch
+    case 13: hipLaunchKernelGGL((sph_sort_head_kernel<13>), dim3(tiles), dim3(1024), 0, s, b.lookup, bin); break;
+    case 12: hipLaunchKernelGGL((sph_sort_head_kernel<12>), dim3(tiles), dim3(512), 0, s, b.lookup, bin); break;
+    case 11: hipLaunchKernelGGL((sph_sort_head_kernel<11>), dim3(tiles), dim3(256), 0, s, b.lookup, bin); break;
+    default:  // P < 2048: one tile of P entries
+      e = launch_sort_local(kmax, true, tiles, lt, s, b.lookup, tile, 0u, first_global_stage - 1u, 0u, bin);
+      if (e != hipSuccess) return e;
+  }
+  e = hipGetLastError();
   ++*launches;
   if (e != hipSuccess) return e;
   for (uint32_t stage = first_global_stage; stage < stages; ++stage) {

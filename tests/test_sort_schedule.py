@@ -1,0 +1,168 @@
+"""The static sort schedules of rps_kernels.hip (sph_sort_head_kernel / sph_sort_tail_kernel),
+replayed on the host with numpy: every lane's registers, the LDS tile (logical indices), the
+DPP partners and the register chunks, exactly as the kernels index them.  They must equal the
+reference's pass-per-dispatch bitonic network (compute_shader.wgsl:470-505 with the pass table of
+src/particle_compute.rs:117-149) on a tile, including the order of equal keys, which the
+network fixes (the payload is the original position).  CPU only: this pins the schedule
+arithmetic; the GPU tests pin the kernels (test_gpu_sph.py)."""
+import numpy as np
+import pytest
+
+
+def ref_network(keys, stages, first_stage=0, first_step=None):
+    """(key, payload) pairs sorted by the reference's passes of stages [first_stage, stages)."""
+    a = np.stack([keys, np.arange(len(keys))], 1).astype(np.int64)
+    n = len(a)
+    for stage in range(first_stage, stages):
+        step0 = 0 if first_step is None or stage != first_stage else first_step
+        for step in range(step0, stage + 1):
+            G = 1 << (stage - step)
+            flip = step == 0
+            i = np.arange(n // 2)
+            h = i % G
+            left = h + 2 * G * (i // G)
+            right = left + (2 * G - 1 - 2 * h if flip else G)
+            sw = a[left, 0] > a[right, 0]
+            l, r = a[left[sw]].copy(), a[right[sw]].copy()
+            a[left[sw]], a[right[sw]] = r, l
+    return a
+
+
+def cas(v, i, j):
+    """v: (threads, 8, 2) lane registers; compare-swap entries i, j of every lane."""
+    sw = v[:, i, 0] > v[:, j, 0]
+    a, b = v[sw, i].copy(), v[sw, j].copy()
+    v[sw, i], v[sw, j] = b, a
+
+
+def group_passes(v, K):
+    M = 1 << K
+    for m in range(K - 1, -1, -1):
+        for j in range(M):
+            if not j & (1 << m):
+                cas(v, j, j + (1 << m))
+
+
+def xlane(v, partner, rev, left):
+    p = v[partner][:, ::-1] if rev else v[partner]
+    p = p.copy()
+    sw = np.where(left[:, None], v[:, :, 0] > p[:, :, 0], p[:, :, 0] > v[:, :, 0])
+    v[sw] = p[sw]
+
+
+def lds_chunk(lds, nt, LG, K):
+    LGG = LG - K + 1
+    g = 1 << LGG
+    NG = 1 << (3 - K)
+    for i in range(NG):
+        q = np.arange(nt) * NG + i
+        e0 = ((q >> LGG) << (LG + 1)) + (q & (g - 1))
+        idx = e0[:, None] + np.arange(1 << K)[None, :] * g
+        v = lds[idx].copy()
+        group_passes(v, K)
+        lds[idx] = v
+
+
+def tail(tile, TLOG):
+    nt = 1 << (TLOG - 3)
+    t = np.arange(nt)
+    v = tile[t[:, None] + np.arange(8)[None, :] * nt].copy()
+    group_passes(v, 3)
+    lds = np.zeros_like(tile)
+    lds[t[:, None] + np.arange(8)[None, :] * nt] = v
+    LG = TLOG - 4
+    while LG >= 4:
+        K = 3 if LG - 3 >= 3 else LG - 3
+        lds_chunk(lds, nt, LG, K)
+        LG -= K
+    v = lds[8 * t[:, None] + np.arange(8)[None, :]].copy()
+    xlane(v, t ^ 1, False, (t & 1) == 0)
+    group_passes(v, 3)
+    return v.reshape(-1, 2)
+
+
+def head(tile, TLOG):
+    nt = 1 << (TLOG - 3)
+    t = np.arange(nt)
+    v = tile.reshape(nt, 8, 2).copy()
+    for i in range(0, 8, 2):
+        cas(v, i, i + 1)
+    for b in (0, 4):
+        cas(v, b, b + 3)
+        cas(v, b + 1, b + 2)
+    for i in range(0, 8, 2):
+        cas(v, i, i + 1)
+    for j in range(4):
+        cas(v, j, 7 - j)
+    for b in (0, 4):
+        cas(v, b, b + 2)
+        cas(v, b + 1, b + 3)
+    for i in range(0, 8, 2):
+        cas(v, i, i + 1)
+    xlane(v, t ^ 1, True, (t & 1) == 0)  # stage 3
+    group_passes(v, 3)
+    xlane(v, t ^ 3, True, (t & 2) == 0)  # stage 4
+    xlane(v, t ^ 1, False, (t & 1) == 0)
+    group_passes(v, 3)
+    lds = np.zeros_like(tile)
+    own = 8 * t[:, None] + np.arange(8)[None, :]
+    for S in range(5, TLOG):
+        lds[own] = v
+        g = 1 << (S - 1)
+        LP = S - 2
+        base = (t >> LP) << (S + 1)
+        r = t & ((1 << LP) - 1)
+        ia = base[:, None] + r[:, None] + np.arange(4)[None, :] * g
+        ib = base[:, None] + (g - 1 - r)[:, None] + np.arange(4)[None, :] * g
+        w = np.concatenate([lds[ia], lds[ib]], 1)
+        for j in range(2):
+            cas(w, j, 7 - j)
+            cas(w, 4 + j, 3 - j)
+        for c in (0, 4):
+            cas(w, c, c + 1)
+            cas(w, c + 2, c + 3)
+        lds[ia], lds[ib] = w[:, :4], w[:, 4:]
+        LG = S - 2
+        while LG >= 5:
+            K = 3 if LG - 4 >= 3 else LG - 4
+            lds_chunk(lds, nt, LG, K)
+            LG -= K
+        v = lds[own].copy()
+        if S >= 6:
+            xlane(v, t ^ 2, False, (t & 2) == 0)
+        xlane(v, t ^ 1, False, (t & 1) == 0)
+        group_passes(v, 3)
+    return v.reshape(-1, 2)
+
+
+@pytest.mark.parametrize("TLOG", [11, 12, 13])
+@pytest.mark.parametrize("kmax", [7, 1 << 20])
+def test_head_schedule_equals_network(TLOG, kmax):
+    g = np.random.default_rng(TLOG * 7 + (kmax & 3))
+    keys = g.integers(0, kmax, 1 << TLOG)  # kmax 7: dense ties; 2^20: mostly distinct
+    tile = np.stack([keys, np.arange(len(keys))], 1).astype(np.int64)
+    np.testing.assert_array_equal(head(tile, TLOG), ref_network(keys, TLOG))
+
+
+@pytest.mark.parametrize("TLOG", [11, 12, 13])
+@pytest.mark.parametrize("kmax", [7, 1 << 20])
+def test_tail_schedule_equals_network(TLOG, kmax):
+    """A later stage s's passes inside one tile: strides 2^(TLOG-1) .. 1, non-flip (the tile
+    after the stage's global passes; any input order)."""
+    g = np.random.default_rng(TLOG * 11 + (kmax & 5))
+    keys = g.integers(0, kmax, 1 << TLOG)
+    tile = np.stack([keys, np.arange(len(keys))], 1).astype(np.int64)
+    # the reference's stage-(TLOG) passes from step 1 (stride 2^(TLOG-1)) on a tile of 2^TLOG:
+    # ref_network over stages [TLOG, TLOG+1) would need 2^(TLOG+1) entries, so run the non-flip
+    # passes directly.
+    a = tile.copy()
+    n = len(a)
+    for lg in range(TLOG - 1, -1, -1):
+        G = 1 << lg
+        i = np.arange(n // 2)
+        left = i % G + 2 * G * (i // G)
+        right = left + G
+        sw = a[left, 0] > a[right, 0]
+        l, r = a[left[sw]].copy(), a[right[sw]].copy()
+        a[left[sw]], a[right[sw]] = r, l
+    np.testing.assert_array_equal(tail(tile, TLOG), a)

@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 for n in 4194304 1048576 524288; do
   echo "== ab n=$n"
-  timeout -k 10 300 python3 tools/ab_sph.py --n $n --frames 50 --rounds 3 ablibs/base/librps.so ablibs/tail/librps.so > gpurun_out/ab_sort_$n.log 2>&1 || { cat gpurun_out/ab_sort_$n.log; exit 1; }
+  timeout -k 10 300 python3 tools/ab_sph.py --n $n --frames 50 --rounds 3 ablibs/base/librps.so ablibs/tail/librps.so ablibs/pairs/librps.so ablibs/head/librps.so > gpurun_out/ab_sort_$n.log 2>&1 || { cat gpurun_out/ab_sort_$n.log; exit 1; }
   cat gpurun_out/ab_sort_$n.log
 done
 echo "== prof sph 2^22"
