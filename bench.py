@@ -194,6 +194,15 @@ def pmc_traffic(workload_name):
         return None
 
 
+def pmc_sph():
+    """The SPH frame's measured per-kernel traffic (tools/collect_sph_traffic.py), or None."""
+    try:
+        with open(PMC_FILE) as f:
+            return json.load(f).get("SPH-2^22-frame")
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(rps, args, cfg, ext):
     """The oracle's OpenMP build (same f32 semantics as the kernel) on the host cores, on a
     bounded sample of the workload: the same per-particle step over `cpu_sample` particles
@@ -363,6 +372,12 @@ def sph_side(rps, args, d):
     sim_ms = d.max(sim_ms)
     frame_ms = el * 1e3 / args.sph_frames
     sim_gbps = cost["sim_bytes"] / (sim_ms * 1e-3) / 1e9
+    # Measured traffic (PMC, the bench workload at 2^22; profiles/pmc_traffic.json): the sim
+    # kernel's L1 -> L2 request bytes, and every SPH kernel's memory-side bytes per frame.
+    pmc = pmc_sph() if n == 1 << 22 else None
+    sim_pmc = next((v for k, v in (pmc or {}).get("per_dispatch", {}).items() if k.startswith("sph_sim_kernel")), None)
+    sim_traffic = sim_pmc["l2_read_bytes"] + sim_pmc["l2_write_bytes"] if sim_pmc else None
+    hbm_frame = (pmc or {}).get("frame_sum_of_kernels", {}).get("hbm_bytes")
     pow2 = n & (n - 1) == 0
     layout = os.environ.get("RPS_SPH_LAYOUT", "1")
     spatial = pow2 and (layout == "2" or (layout == "1" and n >= (1 << 21)))  # rps_context.hip
@@ -372,12 +387,22 @@ def sph_side(rps, args, d):
            "particle_steps_per_s": float(n) * d.world * args.sph_frames / el,
            "sim_kernel_ms": sim_ms,
            "roofline": {"bound": "l2", "kernel": "sph_sim_kernel", "achieved": sim_gbps, "peak": L2_PEAK_GBPS,
-                        "unit": "GB/s", "frac": sim_gbps / L2_PEAK_GBPS, "traffic": None,
+                        "unit": "GB/s", "frac": sim_gbps / L2_PEAK_GBPS, "traffic": sim_traffic,
+                        "traffic_gbps": sim_traffic / (sim_ms * 1e-3) / 1e9 if sim_traffic else None,
+                        "traffic_frac": sim_traffic / (sim_ms * 1e-3) / 1e9 / L2_PEAK_GBPS if sim_traffic else None,
                         "algorithmic_bytes_per_launch": cost["sim_bytes"],
                         "scanned_entries_per_particle": cost["scanned_entries"] / cost["slots"],
-                        "within_radius_per_particle": cost["within_entries"] / cost["slots"]},
+                        "within_radius_per_particle": cost["within_entries"] / cost["slots"],
+                        "note": "achieved/frac: the algorithmic bytes (every neighbour gather charged; most are "
+                                "served by the L1s) per kernel time, as a rate against the aggregate L2 peak -- "
+                                "not an L2 utilisation; traffic: the L1 -> L2 request bytes the PMC counters "
+                                "measured per launch (profiles/pmc_traffic.json), traffic_frac its rate against "
+                                "the same peak"},
            "frame_cost": {"bytes": cost["frame_bytes"], "gbps": cost["frame_bytes"] / (frame_ms * 1e-3) / 1e9,
                           "frac_of_l2": cost["frame_bytes"] / (frame_ms * 1e-3) / 1e9 / L2_PEAK_GBPS,
+                          "hbm_bytes_measured": hbm_frame,
+                          "hbm_gbps_measured": hbm_frame / (frame_ms * 1e-3) / 1e9 if hbm_frame else None,
+                          "hbm_frac_measured": hbm_frame / (frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS if hbm_frame else None,
                           "sort_launches": cost["sort_launches"]}}
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline and args.sph_cpu_n > 0:
         out["cpu_baseline"] = sph_cpu_baseline(rps, args)

@@ -147,7 +147,7 @@ int env_int(const char* name, int dflt) {
 // stores) from the 32 B/particle of state the step streams.  Nontemporal stores always;
 // loads temporal while the state is within about twice the 256-MB Infinity Cache (MALL),
 // which then still serves part of each step's reads.  Same box, C2 ext, us/step, both
-// nontemporal vs temporal loads (tools/ab_stream.py AB_C2=1 AB_N=n RPS_STREAM_NT=3/2):
+// nontemporal vs temporal loads (round 2, tools/ab_stream.py with the since-removed NT knob):
 //   2^20 (32 MiB) 6.00 / 6.44     2^21 11.25 / 9.48     2^22 22.37 / 21.29
 //   2^23 42.89 / 39.38            2^24 (512 MiB) 82.48 / 75.03
 //   20 Mi (640 MiB) 102.8 / 107.0 24 Mi 122.3 / 131.3   2^25 162.1 / 176.0   1e8 479 / 522

@@ -1145,6 +1145,95 @@ __global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_e
   for (int i = 0; i < 4; ++i) out[i] = make_uint4(v[2 * i].x, v[2 * i].y, v[2 * i + 1].x, v[2 * i + 1].y);
 }
 
+// ---------------------------------------------------------------------------------------
+// Static-network gathered-tile launch: all T >= 5 global passes of one stage (strides 2^s down to
+// the local tile 2^lg) in one launch, like sph_sort_stage_kernel below, with the schedule fixed at
+// compile time.  A workgroup gathers the residues r0 .. r0 + W - 1 (and their mirrors g - W - r0
+// .. g - 1 - r0) of every class j < 2^T: in tile order tau = 2W j + W c + k the stage's passes
+// are the tile's stage T + LW from its flip down to stride 2W.  The flip chunk (flip + the next
+// stride) loads its eight entries straight from the lookup, the last chunk stores straight to
+// it, the chunks between run in LDS with compile-time addresses.
+// ---------------------------------------------------------------------------------------
+
+// A non-flip register chunk read from LDS, stored through `store(tau, entry)`.
+template <int LG, int K, class Store>
+__device__ __forceinline__ void lds_chunk_out(const uint2* lds, uint32_t t, Store&& store) {
+  constexpr int LGG = LG - K + 1;
+  constexpr uint32_t g = 1u << LGG;
+  constexpr int NG = 1 << (3 - K);
+#pragma unroll
+  for (int i = 0; i < NG; ++i) {
+    const uint32_t q = t * NG + i;
+    const uint32_t e0 = ((q >> LGG) << (LG + 1)) + (q & (g - 1u));
+    const uint32_t a = padded(e0);
+    uint2 v[1 << K];
+#pragma unroll
+    for (int j = 0; j < (1 << K); ++j) v[j] = lds[a + pad_off<g>(j)];
+    group_passes<K>(v);
+#pragma unroll
+    for (int j = 0; j < (1 << K); ++j) store(e0 + j * g, v[j]);
+  }
+}
+
+// Non-flip strides 2^LG down to 2^LO in LDS chunks of up to three passes, the lowest chunk
+// (up to three passes) left for lds_chunk_out.
+template <int LG, int LO>
+__device__ __forceinline__ void gather_mid_chunks(uint2* lds, uint32_t t) {
+  constexpr int left = LG - LO + 1;  // passes from 2^LG down to 2^LO
+  if constexpr (left > 3) {
+    constexpr int K = (left - 3) % 3 == 0 ? 3 : (left - 3) % 3;
+    lds_chunk<LG, K>(lds, t);
+    __syncthreads();
+    gather_mid_chunks<LG - K, LO>(lds, t);
+  }
+}
+
+template <int T, int LW>
+__global__ __launch_bounds__(1u << (T + LW - 2)) __attribute__((amdgpu_waves_per_eu(4))) void sph_sort_gather_kernel(
+    uint2* __restrict__ lookup, uint32_t s, uint32_t lg) {
+  static_assert(T >= 5 && T + LW + 1 <= 13, "eight entries per thread, at most 1024 threads");
+  constexpr int TL = T + LW + 1;  // log2 of the gathered tile
+  constexpr uint32_t TT = 1u << TL, W = 1u << LW, gp = TT / 4;
+  __shared__ uint2 lds[TT + TT / 32];
+  const uint32_t g = 1u << lg;
+  const uint32_t rgs = lg - LW - 1u;  // log2(residue groups of W in [0, g/2))
+  const uint32_t base = (blockIdx.x >> rgs) << (s + 1u);
+  const uint32_t r0 = (blockIdx.x & ((1u << rgs) - 1u)) << LW;
+  const auto pos = [&](uint32_t tau) {
+    const uint32_t j = tau >> (LW + 1), c = (tau >> LW) & 1u, k = tau & (W - 1u);
+    return base + j * g + (c ? (g - W - r0 + k) : (r0 + k));
+  };
+  const uint32_t t = threadIdx.x;
+  {  // the flip (G' = TT/2) and stride TT/4 on class t and its mirror gp - 1 - t, from memory
+    uint2 v[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[j] = lookup[pos(t + j * gp)];
+      v[4 + j] = lookup[pos(gp - 1u - t + j * gp)];
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      cas(v[j], v[7 - j]);
+      cas(v[4 + j], v[3 - j]);
+    }
+#pragma unroll
+    for (int c = 0; c < 8; c += 4) {
+      cas(v[c], v[c + 1]);
+      cas(v[c + 2], v[c + 3]);
+    }
+    const uint32_t a = padded(t), b = padded(gp - 1u - t);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      lds[a + pad_off<gp>(j)] = v[j];
+      lds[b + pad_off<gp>(j)] = v[4 + j];
+    }
+  }
+  __syncthreads();
+  gather_mid_chunks<TL - 3, LW + 1>(lds, t);  // strides TT/8 .. 2W, all but the last chunk
+  constexpr int KL = T - 2 >= 3 ? 3 : T - 2;
+  lds_chunk_out<LW + KL, KL>(lds, t, [&](uint32_t tau, uint2 e) { lookup[pos(tau)] = e; });
+}
+
 // All T global passes of one stage in one launch (T > 4 would take two or more register-fused
 // launches).  The passes have strides G = 2^s down to g = 2^lg (the LDS tile of the local
 // launches); as in sort_group, residue class r (positions r + j*g of a 2G block, j < 2^T)
@@ -2286,15 +2375,17 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
     // Stages with five or more global passes run them all in one gathered-tile launch
     // (sph_sort_stage_kernel).
     if (step < T && T >= 5u && T <= 9u && tile_log >= 6u) {
-      const uint32_t tt = 32u << T;
-      const uint32_t blocks = (P >> (stage + 1u)) << (tile_log - 5u);
-      const uint32_t threads = std::max(64u, std::min(1024u, tt >> 3));
-      if (tt > kSortTile)
-        hipLaunchKernelGGL((sph_sort_stage_kernel<3, kSortTileMax>), dim3(blocks), dim3(threads), 0, s,
-                           b.lookup, stage, tile_log, T);
-      else
-        hipLaunchKernelGGL((sph_sort_stage_kernel<3, kSortTile>), dim3(blocks), dim3(threads), 0, s,
-                           b.lookup, stage, tile_log, T);
+      // Residue groups of 16 (of 8 at T = 9, so the gathered tile stays 8192 entries).
+      const uint32_t lw = T == 9u ? 3u : 4u;
+      const uint32_t blocks = (P >> (stage + 1u)) << (tile_log - lw - 1u);
+      const uint32_t threads = (2u << (T + lw)) / 8u;
+      switch (T) {
+        case 5: hipLaunchKernelGGL((sph_sort_gather_kernel<5, 4>), dim3(blocks), dim3(threads), 0, s, b.lookup, stage, tile_log); break;
+        case 6: hipLaunchKernelGGL((sph_sort_gather_kernel<6, 4>), dim3(blocks), dim3(threads), 0, s, b.lookup, stage, tile_log); break;
+        case 7: hipLaunchKernelGGL((sph_sort_gather_kernel<7, 4>), dim3(blocks), dim3(threads), 0, s, b.lookup, stage, tile_log); break;
+        case 8: hipLaunchKernelGGL((sph_sort_gather_kernel<8, 4>), dim3(blocks), dim3(threads), 0, s, b.lookup, stage, tile_log); break;
+        default: hipLaunchKernelGGL((sph_sort_gather_kernel<9, 3>), dim3(blocks), dim3(threads), 0, s, b.lookup, stage, tile_log); break;
+      }
       e = hipGetLastError();
       ++*launches;
       if (e != hipSuccess) return e;

@@ -166,3 +166,73 @@ def test_tail_schedule_equals_network(TLOG, kmax):
         l, r = a[left[sw]].copy(), a[right[sw]].copy()
         a[left[sw]], a[right[sw]] = r, l
     np.testing.assert_array_equal(tail(tile, TLOG), a)
+
+
+def ref_passes(a, stage, steps):
+    """The reference's passes (stage, step) for step in steps, on (key, payload) rows."""
+    a = a.copy()
+    n = len(a)
+    for step in steps:
+        G = 1 << (stage - step)
+        flip = step == 0
+        i = np.arange(n // 2)
+        h = i % G
+        left = h + 2 * G * (i // G)
+        right = left + (2 * G - 1 - 2 * h if flip else G)
+        sw = a[left, 0] > a[right, 0]
+        l, r = a[left[sw]].copy(), a[right[sw]].copy()
+        a[left[sw]], a[right[sw]] = r, l
+    return a
+
+
+def gather_stage(a, s, lg, T, LW):
+    """sph_sort_gather_kernel<T, LW> over every workgroup (rps_kernels.hip)."""
+    a = a.copy()
+    P = len(a)
+    TL = T + LW + 1
+    TT, W, gp = 1 << TL, 1 << LW, 1 << (TL - 2)
+    nt = TT // 8
+    g = 1 << lg
+    rgs = lg - LW - 1
+    blocks = (P >> (s + 1)) << rgs
+    t = np.arange(nt)
+    for blk in range(blocks):
+        base = (blk >> rgs) << (s + 1)
+        r0 = (blk & ((1 << rgs) - 1)) << LW
+        tau = np.arange(TT)
+        j, c, k = tau >> (LW + 1), (tau >> LW) & 1, tau & (W - 1)
+        pos = base + j * g + np.where(c == 1, g - W - r0 + k, r0 + k)
+        lds = a[pos].copy()
+        ia = t[:, None] + np.arange(4)[None, :] * gp
+        ib = (gp - 1 - t)[:, None] + np.arange(4)[None, :] * gp
+        v = np.concatenate([lds[ia], lds[ib]], 1)
+        for jj in range(2):
+            cas(v, jj, 7 - jj)
+            cas(v, 4 + jj, 3 - jj)
+        for cc in (0, 4):
+            cas(v, cc, cc + 1)
+            cas(v, cc + 2, cc + 3)
+        lds[ia], lds[ib] = v[:, :4], v[:, 4:]
+        LG, LO = TL - 3, LW + 1
+        while LG - LO + 1 > 3:
+            left = LG - LO + 1
+            K = 3 if (left - 3) % 3 == 0 else (left - 3) % 3
+            lds_chunk(lds, nt, LG, K)
+            LG -= K
+        lds_chunk(lds, nt, LG, LG - LO + 1)  # the last chunk (stored to memory by the kernel)
+        a[pos] = lds
+    return a
+
+
+@pytest.mark.parametrize("T,LW", [(5, 4), (6, 4), (7, 4), (8, 4), (9, 3)])
+@pytest.mark.parametrize("kmax", [5, 1 << 20])
+def test_gather_stage_schedule_equals_network(T, LW, kmax):
+    """A stage's T global passes (local tiles of 2^lg entries, stage s = lg + T - 1) as the
+    gathered-tile launch runs them, against the reference's passes of that stage on the array."""
+    lg = LW + 2
+    s = lg + T - 1
+    P = 1 << (s + 2)
+    g = np.random.default_rng(T * 13 + LW + (kmax & 7))
+    keys = g.integers(0, kmax, P)
+    a = np.stack([keys, np.arange(P)], 1).astype(np.int64)
+    np.testing.assert_array_equal(gather_stage(a, s, lg, T, LW), ref_passes(a, s, range(T)))

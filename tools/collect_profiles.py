@@ -66,9 +66,12 @@ def main(tag):
                                      "round": tag}
     with open(os.path.join(PROF, f"{tag}_kernel_summary.json"), "w") as f:
         json.dump({"trace": summary, "pmc": pmc}, f, indent=1, sort_keys=True)
-    if traffic:
-        with open(os.path.join(PROF, "pmc_traffic.json"), "w") as f:
-            json.dump(traffic, f, indent=1, sort_keys=True)
+    if traffic:  # merged into the file (it also holds the SPH entry, tools/collect_sph_traffic.py)
+        path = os.path.join(PROF, "pmc_traffic.json")
+        old = json.load(open(path)) if os.path.exists(path) else {}
+        old.update(traffic)
+        with open(path, "w") as f:
+            json.dump(old, f, indent=1, sort_keys=True)
     print(json.dumps({"trace": {k[:90]: v for k, v in summary.items()}, "traffic": traffic}, indent=1))
 
 
