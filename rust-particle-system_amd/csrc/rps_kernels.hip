@@ -639,6 +639,12 @@ __global__ __launch_bounds__(kBlock) void sph_sort_fused_kernel(uint2* __restric
   sort_group<K, FLIP>(lookup, base, r, g);
 }
 
+#ifndef RPS_HEAD_TPW
+#define RPS_HEAD_TPW 2
+#endif
+#ifndef RPS_TAIL_TPW
+#define RPS_TAIL_TPW 2
+#endif
 constexpr uint32_t kSortTile = 8192;      // entries per workgroup tile (64 KiB of LDS)
 constexpr uint32_t kSortTileMax = 16384;  // largest tile (132 KiB of LDS, one workgroup per CU)
 constexpr uint32_t kSortLd = 8;           // 16-B tile loads a lane keeps in flight at once
@@ -921,42 +927,58 @@ __device__ __forceinline__ void lds_chunks(uint2* lds, uint32_t t) {
   }
 }
 
-template <int TLOG>
+// TPW tiles per workgroup, one after the other: the next tile's first-chunk loads are issued
+// before this tile's passes and land while they run, and this tile's stores drain while the
+// next one's run.  (One tile per workgroup puts the whole chip through load, LDS passes and
+// store in step: 19.5 us at 2^22 for what a register-fused launch moves in 10.4.)
+template <int TLOG, int TPW>
 __global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_eu(4))) void sph_sort_tail_kernel(uint2* __restrict__ lookup) {
   static_assert(TLOG >= 10 && TLOG <= 13, "eight entries per thread, 128..1024 threads");
   constexpr uint32_t TILE = 1u << TLOG, NT = TILE / 8;
   __shared__ uint2 lds[TILE + TILE / 32];
   const uint32_t t = threadIdx.x;
-  uint2* tile = lookup + (size_t)blockIdx.x * TILE;
-  {  // strides TILE/2, TILE/4, TILE/8: group r = t, entries t + j * NT, straight from the lookup
-    uint2 v[8];
+  uint2* tile = lookup + (size_t)blockIdx.x * TPW * TILE;
+  uint2 v[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = tile[t + j * NT];
-    group_passes<3>(v);
-    const uint32_t a = padded(t);
+  for (int j = 0; j < 8; ++j) v[j] = tile[t + j * NT];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) lds[a + pad_off<NT>(j)] = v[j];
-  }
-  __syncthreads();
-  lds_chunks<TLOG - 4>(lds, t);
-  {  // strides 8, 4, 2, 1: lane pair (2k, 2k + 1) holds the 16 entries [16k, 16k + 16)
-    const uint32_t a = padded(8u * t);
-    uint2 v[8];
+  for (int k = 0; k < TPW; ++k, tile += TILE) {
+    uint2 nxt[8];
+    if (k + 1 < TPW) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = lds[a + i];
-    const bool left = (t & 1u) == 0u;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {  // stride 8: entry i of the left lane against entry i of the right
-      uint2 p;
-      p.x = (uint32_t)__builtin_amdgcn_mov_dpp((int)v[i].x, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
-      p.y = (uint32_t)__builtin_amdgcn_mov_dpp((int)v[i].y, 0xB1, 0xF, 0xF, false);
-      const bool swap = left ? (v[i].x > p.x) : (p.x > v[i].x);
-      v[i] = swap ? p : v[i];
+      for (int j = 0; j < 8; ++j) nxt[j] = tile[TILE + t + j * NT];
     }
-    group_passes<3>(v);  // strides 4, 2, 1 inside the lane's eight
-    uint4* out = reinterpret_cast<uint4*>(tile + 8u * t);
+    {  // strides TILE/2, TILE/4, TILE/8: group r = t, entries t + j * NT, straight from the lookup
+      group_passes<3>(v);
+      const uint32_t a = padded(t);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) out[i] = make_uint4(v[2 * i].x, v[2 * i].y, v[2 * i + 1].x, v[2 * i + 1].y);
+      for (int j = 0; j < 8; ++j) lds[a + pad_off<NT>(j)] = v[j];
+    }
+    __syncthreads();
+    lds_chunks<TLOG - 4>(lds, t);
+    {  // strides 8, 4, 2, 1: lane pair (2k, 2k + 1) holds the 16 entries [16k, 16k + 16)
+      const uint32_t a = padded(8u * t);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = lds[a + i];
+      const bool left = (t & 1u) == 0u;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {  // stride 8: entry i of the left lane against entry i of the right
+        uint2 p;
+        p.x = (uint32_t)__builtin_amdgcn_mov_dpp((int)v[i].x, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
+        p.y = (uint32_t)__builtin_amdgcn_mov_dpp((int)v[i].y, 0xB1, 0xF, 0xF, false);
+        const bool swap = left ? (v[i].x > p.x) : (p.x > v[i].x);
+        v[i] = swap ? p : v[i];
+      }
+      group_passes<3>(v);  // strides 4, 2, 1 inside the lane's eight
+      uint4* out = reinterpret_cast<uint4*>(tile + 8u * t);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) out[i] = make_uint4(v[2 * i].x, v[2 * i].y, v[2 * i + 1].x, v[2 * i + 1].y);
+    }
+    if (k + 1 < TPW) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = nxt[j];
+      __syncthreads();  // every wave has read this tile's LDS image before the next one's writes
+    }
   }
 }
 
@@ -1090,59 +1112,84 @@ __device__ __forceinline__ void head_stages(uint2* lds, uint32_t t, uint2 (&v)[8
   }
 }
 
-template <int TLOG>
+// The bin pass's inputs for a tile (entry pairs q = 2t + 2k*NT): positions, or the previous
+// frame's pad entries [n, P) (the reference never rewrites them).
+struct BinLoads {
+  f2 pa[4], pc[4];
+  uint4 lk[4];
+};
+template <uint32_t NT>
+__device__ __forceinline__ void bin_load(const uint2* lookup, const SortBin& bin, uint32_t base0, uint32_t t,
+                                         BinLoads& in) {
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k) {
+    const uint32_t gq = base0 + 2u * t + k * 2u * NT;
+    if (gq < bin.n) {
+      in.pa[k] = bin_pos(bin, gq);
+      if (gq + 1u < bin.n) in.pc[k] = bin_pos(bin, gq + 1u);
+      else in.lk[k] = *reinterpret_cast<const uint4*>(lookup + gq);
+    } else {
+      in.lk[k] = *reinterpret_cast<const uint4*>(lookup + gq);
+    }
+  }
+}
+template <uint32_t NT>
+__device__ __forceinline__ void bin_keys(const SortBin& bin, uint32_t base0, uint32_t t, const BinLoads& in,
+                                         const PaddedTile& s) {
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k) {
+    const uint32_t q = 2u * t + k * 2u * NT, gq = base0 + q;
+    uint2 a, c;
+    if (gq < bin.n) {
+      a = bin_key(bin, in.pa[k], gq);
+      c = gq + 1u < bin.n ? bin_key(bin, in.pc[k], gq + 1u) : make_uint2(in.lk[k].z, in.lk[k].w);
+    } else {
+      a = make_uint2(in.lk[k].x, in.lk[k].y);
+      c = make_uint2(in.lk[k].z, in.lk[k].w);
+    }
+    s[q] = a;
+    s[q + 1u] = c;
+  }
+}
+
+// TPW tiles per workgroup, one after the other, the next tile's bin inputs loaded before this
+// tile's stages (as in the tail launch).
+template <int TLOG, int TPW>
 __global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_eu(4))) void sph_sort_head_kernel(uint2* __restrict__ lookup, SortBin bin) {
   static_assert(TLOG >= 10 && TLOG <= 13, "eight entries per thread, 128..1024 threads");
   constexpr uint32_t TILE = 1u << TLOG, NT = TILE / 8;
   __shared__ uint2 lds[TILE + TILE / 32];
   const PaddedTile s{lds};
   const uint32_t t = threadIdx.x;
-  const uint32_t base0 = blockIdx.x * TILE;
-  {  // bin: entry pairs q = 2t + 2k*NT, every position (or pad entry) load first, then the keys
-    f2 pa[4], pc[4];
-    uint4 lk[4];
+  uint32_t base0 = blockIdx.x * TPW * TILE;
+  BinLoads in;
+  bin_load<NT>(lookup, bin, base0, t, in);
 #pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {
-      const uint32_t gq = base0 + 2u * t + k * 2u * NT;
-      if (gq < bin.n) {
-        pa[k] = bin_pos(bin, gq);
-        if (gq + 1u < bin.n) pc[k] = bin_pos(bin, gq + 1u);
-        else lk[k] = *reinterpret_cast<const uint4*>(lookup + gq);
-      } else {
-        lk[k] = *reinterpret_cast<const uint4*>(lookup + gq);
-      }
-    }
+  for (int k = 0; k < TPW; ++k, base0 += TILE) {
+    BinLoads nxt;
+    if (k + 1 < TPW) bin_load<NT>(lookup, bin, base0 + TILE, t, nxt);
+    bin_keys<NT>(bin, base0, t, in, s);
+    __syncthreads();
+    uint2 v[8];
+    const uint32_t a = padded(8u * t);
 #pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {
-      const uint32_t q = 2u * t + k * 2u * NT, gq = base0 + q;
-      uint2 a, c;
-      if (gq < bin.n) {
-        a = bin_key(bin, pa[k], gq);
-        c = gq + 1u < bin.n ? bin_key(bin, pc[k], gq + 1u) : make_uint2(lk[k].z, lk[k].w);
-      } else {
-        a = make_uint2(lk[k].x, lk[k].y);
-        c = make_uint2(lk[k].z, lk[k].w);
-      }
-      s[q] = a;
-      s[q + 1u] = c;
+    for (int i = 0; i < 8; ++i) v[i] = lds[a + i];
+    reg_stages012(v);
+    xlane_pass<kDppXor1, true>(v, (t & 1u) == 0u);  // stage 3: flip G = 8 (lane pair), then 4, 2, 1
+    group_passes<3>(v);
+    xlane_pass<kDppRev4, true>(v, (t & 2u) == 0u);  // stage 4: flip G = 16 (lane quad), then 8 ... 1
+    reg_tail<false>(v, t);
+    // The bin's LDS image was read back by this lane only ([8t, 8t + 8)); its other entries were
+    // written by other waves before the barrier above, so stage 5's first write is safe.
+    head_stages<5, TLOG>(lds, t, v);
+    uint4* out = reinterpret_cast<uint4*>(lookup + base0 + 8u * t);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[i] = make_uint4(v[2 * i].x, v[2 * i].y, v[2 * i + 1].x, v[2 * i + 1].y);
+    if (k + 1 < TPW) {
+      in = nxt;
+      __syncthreads();  // every wave has read this tile's LDS image before the next bin writes
     }
   }
-  __syncthreads();
-  uint2 v[8];
-  const uint32_t a = padded(8u * t);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) v[i] = lds[a + i];
-  reg_stages012(v);
-  xlane_pass<kDppXor1, true>(v, (t & 1u) == 0u);  // stage 3: flip G = 8 (lane pair), then 4, 2, 1
-  group_passes<3>(v);
-  xlane_pass<kDppRev4, true>(v, (t & 2u) == 0u);  // stage 4: flip G = 16 (lane quad), then 8 ... 1
-  reg_tail<false>(v, t);
-  // The bin's LDS image was read back by this lane only ([8t, 8t + 8)); its other entries were
-  // written by other waves before the barrier above, so stage 5's first write is safe.
-  head_stages<5, TLOG>(lds, t, v);
-  uint4* out = reinterpret_cast<uint4*>(lookup + base0 + 8u * t);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) out[i] = make_uint4(v[2 * i].x, v[2 * i].y, v[2 * i + 1].x, v[2 * i + 1].y);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1489,50 +1536,6 @@ __device__ __forceinline__ uint32_t nine_runs(const RunBounds& rb, float px, flo
   return c;
 }
 
-// The nine runs as pairs of storage-adjacent entries: each merged run of len entries is
-// ceil(len / 2) pairs, pair k of a run holding its entries 2k and 2k + 1 (the last pair of an
-// odd run only 2k), so one 16-B load fetches two neighbours.  Table entry per run: {slot of its
-// first entry - 2 * its first pair index, its pair end | its flat-entry end << 16}; a pair p
-// of that run starts at slot 2p + x and flat index 2p - d, d = 2 * (pair end) - (flat end)
-// of the run before (the odd runs so far).  Returns the pair count; *total_out the entries.
-// Only for totals below 2^16 entries (callers fall back to nine_runs beyond).
-template <bool LAYOUT>
-__device__ __forceinline__ uint32_t nine_runs_pairs(const RunBounds& rb, float px, float py, float xoff,
-                                                    float yoff, float r, uint32_t N, RunTable& runs,
-                                                    uint32_t* total_out) {
-  const uint32_t total = nine_runs<LAYOUT>(rb, px, py, xoff, yoff, r, N, runs);
-  *total_out = total;
-  if (total >= 65536u) return 0;
-  uint32_t pairs = 0, fend = 0;
-  for (uint32_t k = 0; fend < total; ++k) {  // rewrite the entry table in place
-    const uint2 e = runs[k][threadIdx.x];  // {slot - flat start, flat end}
-    const uint32_t f0 = fend;
-    fend = e.y;
-    const uint32_t p0 = pairs;
-    pairs += (fend - f0 + 1u) >> 1;
-    runs[k][threadIdx.x] = make_uint2(e.x + f0 - 2u * p0, pairs | (fend << 16));
-  }
-  return pairs;
-}
-
-struct PairCursor {
-  const RunTable& runs;
-  uint32_t r = 0, d = 0;
-  uint2 cur;
-  __device__ explicit PairCursor(const RunTable& t) : runs(t), cur(t[0][threadIdx.x]) {}
-  // Pair p (non-decreasing p < pairs): its first entry's slot and flat index, and whether its
-  // second entry exists.
-  __device__ __forceinline__ uint32_t slot(uint32_t p, uint32_t& f, bool& second) {
-    if (p >= (cur.y & 0xFFFFu)) {  // runs are non-empty: one step suffices
-      d = 2u * (cur.y & 0xFFFFu) - (cur.y >> 16);
-      cur = runs[++r][threadIdx.x];
-    }
-    f = 2u * p - d;
-    second = f + 1u < (cur.y >> 16);
-    return 2u * p + cur.x;
-  }
-};
-
 // Walks the flat index forward: slot(f) for non-decreasing f < total.
 struct RunCursor {
   const RunTable& runs;
@@ -1568,10 +1571,7 @@ struct RunCursor {
 //
 // calculate_density, compute_shader.wgsl:207-254: entries summed in run order, kScanBatch
 // predicted positions in flight per lane across run boundaries.
-// PAIRS: the scan walks pairs of storage-adjacent entries (nine_runs_pairs), one 16-B load per
-// pair instead of one 8-B load per entry -- half the load instructions, and with them the
-// texture-address work that bounds this scan; the same entries in the same order.
-template <int kScanBatch, bool LAYOUT, bool PAIRS>
+template <int kScanBatch, bool LAYOUT>
 __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* __restrict__ cfg,
                                                              RunBounds rb, SphSlots sl, uint32_t p_slots) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
@@ -1581,72 +1581,42 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
   const uint32_t N = cfg->particle_count;
   const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
   __shared__ RunTable runs;
+  const uint32_t total = nine_runs<LAYOUT>(rb, p[0], p[1], cfg->screen_bounds[1],
+                                   cfg->screen_bounds[3], r, N, runs);
+  RunCursor rc(runs);
   float d = 0.0f, nd = 0.0f;
   uint64_t m0 = 0, m1 = 0;
-  uint32_t total;
-  // One neighbour entry at flat index b (calculate_density's loop body, wgsl:238-252).
-  const auto entry = [&](f2 q, uint32_t b) {
-    const float dx = p[0] - q[0], dy = p[1] - q[1];
-    const float sq = dx * dx + dy * dy;
-    if (!(sq > r2)) {
-      if (total <= 128u) {  // otherwise the sim pass scans the runs (masks unused)
-        if (b < 64u) m0 |= 1ull << b;
-        else m1 |= 1ull << (b - 64u);
-      }
-      // Correctly rounded sqrt without the input scaling unless a lane of the wave needs it
-      // (0 < sq < 2^-96: two particles closer than ~1e-14, only ever near the origin):
-      // the same bits as sqrtf (tools/sqrt_check.hip, every input), 2^22 frame
-      // 1.2461 -> 1.2358 ms (same box).
-      const bool tiny = sq > 0.0f && sq < 0x1p-96f;
-      const float dist = __builtin_amdgcn_ballot_w64(tiny) ? sqrtf(sq) : sqrt_rn_unscaled(sq);
-      float k1 = 0.0f, k2 = 0.0f;
-      if (!(dist >= r)) {
-        const float v = r - dist;
-        k1 = (dn * v) * v;
-        k2 = ((ndn * v) * v) * v;
-      }
-      d = d + k1;
-      nd = nd + k2;
-    }
-  };
-  uint32_t pairs = 0;
-  if constexpr (PAIRS)
-    pairs = nine_runs_pairs<LAYOUT>(rb, p[0], p[1], cfg->screen_bounds[1], cfg->screen_bounds[3], r, N, runs,
-                                    &total);
-  else
-    total = nine_runs<LAYOUT>(rb, p[0], p[1], cfg->screen_bounds[1], cfg->screen_bounds[3], r, N, runs);
-  if (PAIRS && total < 65536u) {
-    // kScanBatch / 2 pairs in flight.  A pair's 16-B load may read the 8 B after the last slot
-    // (pp_s is followed by rec_pv in the arena); that half is never used.
-    constexpr int B = kScanBatch / 2;
-    PairCursor pc(runs);
-    for (uint32_t k = 0; k < pairs; k += B) {
-      f4 q[B];
-      uint32_t fb[B];
-      bool two[B];
+  for (uint32_t f = 0; f < total; f += kScanBatch) {
+    f2 q[kScanBatch];
 #pragma unroll
-      for (int u = 0; u < B; ++u) {
-        const uint32_t j = pc.slot(min(k + u, pairs - 1u), fb[u], two[u]);
-        typedef float f4a8 __attribute__((ext_vector_type(4), aligned(8)));
-        q[u] = *reinterpret_cast<const f4a8*>(sl.pp_s + j);
-      }
+    for (int u = 0; u < kScanBatch; ++u) q[u] = sl.pp_s[rc.slot(min(f + u, total - 1u))];
 #pragma unroll
-      for (int u = 0; u < B; ++u) {
-        if (k + u < pairs) {
-          entry(f2{q[u][0], q[u][1]}, fb[u]);
-          if (two[u]) entry(f2{q[u][2], q[u][3]}, fb[u] + 1u);
+    for (int u = 0; u < kScanBatch; ++u) {
+      if (f + u < total) {
+        const float dx = p[0] - q[u][0], dy = p[1] - q[u][1];
+        const float sq = dx * dx + dy * dy;
+        if (!(sq > r2)) {
+          const uint32_t b = f + u;
+          if (total <= 128u) {  // otherwise the sim pass scans the runs (masks unused)
+            if (b < 64u) m0 |= 1ull << b;
+            else m1 |= 1ull << (b - 64u);
+          }
+          // Correctly rounded sqrt without the input scaling unless a lane of the wave needs it
+          // (0 < sq < 2^-96: two particles closer than ~1e-14, only ever near the origin):
+          // the same bits as sqrtf (tools/sqrt_check.hip, every input), 2^22 frame
+          // 1.2461 -> 1.2358 ms (same box).
+          const bool tiny = sq > 0.0f && sq < 0x1p-96f;
+          const float dist = __builtin_amdgcn_ballot_w64(tiny) ? sqrtf(sq) : sqrt_rn_unscaled(sq);
+          float k1 = 0.0f, k2 = 0.0f;
+          if (!(dist >= r)) {
+            const float v = r - dist;
+            k1 = (dn * v) * v;
+            k2 = ((ndn * v) * v) * v;
+          }
+          d = d + k1;
+          nd = nd + k2;
         }
       }
-    }
-  } else {
-    RunCursor rc(runs);
-    for (uint32_t f = 0; f < total; f += kScanBatch) {
-      f2 q[kScanBatch];
-#pragma unroll
-      for (int u = 0; u < kScanBatch; ++u) q[u] = sl.pp_s[rc.slot(min(f + u, total - 1u))];
-#pragma unroll
-      for (int u = 0; u < kScanBatch; ++u)
-        if (f + u < total) entry(q[u], f + u);
     }
   }
   sl.nbr_mask[t] = m0;
@@ -2346,9 +2316,14 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
   const uint32_t lt = std::max(64u, std::min(1024u, tile >> kmax));
   hipError_t e = hipSuccess;
   switch (tile_log) {  // bin + stages [0, tile_log): the static-network head launch
-    case 13: hipLaunchKernelGGL((sph_sort_head_kernel<13>), dim3(tiles), dim3(1024), 0, s, b.lookup, bin); break;
-    case 12: hipLaunchKernelGGL((sph_sort_head_kernel<12>), dim3(tiles), dim3(512), 0, s, b.lookup, bin); break;
-    case 11: hipLaunchKernelGGL((sph_sort_head_kernel<11>), dim3(tiles), dim3(256), 0, s, b.lookup, bin); break;
+    case 13:
+      if (tiles >= 512u && RPS_HEAD_TPW == 2)
+        hipLaunchKernelGGL((sph_sort_head_kernel<13, 2>), dim3(tiles / 2), dim3(1024), 0, s, b.lookup, bin);
+      else
+        hipLaunchKernelGGL((sph_sort_head_kernel<13, 1>), dim3(tiles), dim3(1024), 0, s, b.lookup, bin);
+      break;
+    case 12: hipLaunchKernelGGL((sph_sort_head_kernel<12, 1>), dim3(tiles), dim3(512), 0, s, b.lookup, bin); break;
+    case 11: hipLaunchKernelGGL((sph_sort_head_kernel<11, 1>), dim3(tiles), dim3(256), 0, s, b.lookup, bin); break;
     default:  // P < 2048: one tile of P entries
       e = launch_sort_local(kmax, true, tiles, lt, s, b.lookup, tile, 0u, first_global_stage - 1u, 0u, bin);
       if (e != hipSuccess) return e;
@@ -2406,10 +2381,15 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
       step += k;
     }
     if (step <= stage) {  // the stage's passes inside each tile: strides tile/2 .. 1
+      // Two tiles per workgroup once that still gives every CU a workgroup (P >= 2^22 here).
+      const bool two = tiles >= 512u && RPS_TAIL_TPW == 2;
       switch (tile_log) {
-        case 13: hipLaunchKernelGGL((sph_sort_tail_kernel<13>), dim3(tiles), dim3(1024), 0, s, b.lookup); break;
-        case 12: hipLaunchKernelGGL((sph_sort_tail_kernel<12>), dim3(tiles), dim3(512), 0, s, b.lookup); break;
-        case 11: hipLaunchKernelGGL((sph_sort_tail_kernel<11>), dim3(tiles), dim3(256), 0, s, b.lookup); break;
+        case 13:
+          if (two) hipLaunchKernelGGL((sph_sort_tail_kernel<13, 2>), dim3(tiles / 2), dim3(1024), 0, s, b.lookup);
+          else hipLaunchKernelGGL((sph_sort_tail_kernel<13, 1>), dim3(tiles), dim3(1024), 0, s, b.lookup);
+          break;
+        case 12: hipLaunchKernelGGL((sph_sort_tail_kernel<12, 1>), dim3(tiles), dim3(512), 0, s, b.lookup); break;
+        case 11: hipLaunchKernelGGL((sph_sort_tail_kernel<11, 1>), dim3(tiles), dim3(256), 0, s, b.lookup); break;
         default:
           e = launch_sort_local(kmax, false, tiles, lt, s, b.lookup, tile, stage, stage, step, nobin);
           if (e != hipSuccess) return e;
@@ -2452,10 +2432,10 @@ static hipError_t launch_sph_density(const SphBuffers& b, hipStream_t s) {
   const RunBounds rb = run_bounds(b);
 #define RPS_DENSITY(B)                                                                            \
   if (b.layout)                                                                                   \
-    hipLaunchKernelGGL((sph_density_kernel<B, true, true>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s, \
+    hipLaunchKernelGGL((sph_density_kernel<B, true>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s, \
                        b.cfg, rb, b.sl, b.p);                                               \
   else                                                                                            \
-    hipLaunchKernelGGL((sph_density_kernel<B, false, true>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s, \
+    hipLaunchKernelGGL((sph_density_kernel<B, false>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s, \
                        b.cfg, rb, b.sl, b.p)
   switch (sph_batch(true, b.p, b.batch_d, b.layout)) {
     case 4: RPS_DENSITY(4); break;
