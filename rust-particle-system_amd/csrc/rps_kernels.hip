@@ -639,14 +639,7 @@ __global__ __launch_bounds__(kBlock) void sph_sort_fused_kernel(uint2* __restric
   sort_group<K, FLIP>(lookup, base, r, g);
 }
 
-#ifndef RPS_HEAD_TPW
-#define RPS_HEAD_TPW 2
-#endif
-#ifndef RPS_TAIL_TPW
-#define RPS_TAIL_TPW 2
-#endif
 constexpr uint32_t kSortTile = 8192;      // entries per workgroup tile (64 KiB of LDS)
-constexpr uint32_t kSortTileMax = 16384;  // largest tile (132 KiB of LDS, one workgroup per CU)
 constexpr uint32_t kSortLd = 8;           // 16-B tile loads a lane keeps in flight at once
 constexpr uint32_t kSortLdBin = 4;        // the same in the bin launch (positions + pad entries)
 
@@ -927,73 +920,6 @@ __device__ __forceinline__ void lds_chunks(uint2* lds, uint32_t t) {
   }
 }
 
-// TPW tiles per workgroup, one after the other: the next tile's first-chunk loads are issued
-// before this tile's passes and land while they run, and this tile's stores drain while the
-// next one's run.  (One tile per workgroup puts the whole chip through load, LDS passes and
-// store in step: 19.5 us at 2^22 for what a register-fused launch moves in 10.4.)
-template <int TLOG, int TPW>
-__global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_eu(4))) void sph_sort_tail_kernel(uint2* __restrict__ lookup) {
-  static_assert(TLOG >= 10 && TLOG <= 13, "eight entries per thread, 128..1024 threads");
-  constexpr uint32_t TILE = 1u << TLOG, NT = TILE / 8;
-  __shared__ uint2 lds[TILE + TILE / 32];
-  const uint32_t t = threadIdx.x;
-  uint2* tile = lookup + (size_t)blockIdx.x * TPW * TILE;
-  uint2 v[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = tile[t + j * NT];
-#pragma unroll
-  for (int k = 0; k < TPW; ++k, tile += TILE) {
-    uint2 nxt[8];
-    if (k + 1 < TPW) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) nxt[j] = tile[TILE + t + j * NT];
-    }
-    {  // strides TILE/2, TILE/4, TILE/8: group r = t, entries t + j * NT, straight from the lookup
-      group_passes<3>(v);
-      const uint32_t a = padded(t);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) lds[a + pad_off<NT>(j)] = v[j];
-    }
-    __syncthreads();
-    lds_chunks<TLOG - 4>(lds, t);
-    {  // strides 8, 4, 2, 1: lane pair (2k, 2k + 1) holds the 16 entries [16k, 16k + 16)
-      const uint32_t a = padded(8u * t);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = lds[a + i];
-      const bool left = (t & 1u) == 0u;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {  // stride 8: entry i of the left lane against entry i of the right
-        uint2 p;
-        p.x = (uint32_t)__builtin_amdgcn_mov_dpp((int)v[i].x, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
-        p.y = (uint32_t)__builtin_amdgcn_mov_dpp((int)v[i].y, 0xB1, 0xF, 0xF, false);
-        const bool swap = left ? (v[i].x > p.x) : (p.x > v[i].x);
-        v[i] = swap ? p : v[i];
-      }
-      group_passes<3>(v);  // strides 4, 2, 1 inside the lane's eight
-      uint4* out = reinterpret_cast<uint4*>(tile + 8u * t);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) out[i] = make_uint4(v[2 * i].x, v[2 * i].y, v[2 * i + 1].x, v[2 * i + 1].y);
-    }
-    if (k + 1 < TPW) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = nxt[j];
-      __syncthreads();  // every wave has read this tile's LDS image before the next one's writes
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------
-// Static-network head launch: bin (wgsl:455-468) + every stage whose whole network fits one
-// tile (stages 0 .. TLOG-1), eight entries per thread.  Between stages a thread holds its eight
-// consecutive entries [8t, 8t + 8) in registers, and lane quads the 32 entries [32k, 32k + 32):
-// passes of stride 1, 2, 4 run inside a lane, strides 8 and 16 (and the flips of stages 3
-// and 4) across the quad with DPP moves, so stages 0-4 and the last five passes of every later
-// stage never touch LDS.  A later stage S writes its entries to LDS once, runs its flip chunk
-// (strides 2^S, 2^(S-1)) and its passes of strides 2^(S-2) .. 32 there in register chunks with
-// compile-time addresses, and reads its entries back.  The last stage stores them.  Same
-// compare-swaps in the same order as the reference's pass-per-dispatch schedule.
-// ---------------------------------------------------------------------------------------
-
 // A pass across lanes: entry j of this lane against entry j (REV: 7 - j) of the DPP partner
 // (quad_perm CTRL); `left` = this lane holds the lower position of each pair.
 template <int CTRL, bool REV>
@@ -1013,6 +939,50 @@ __device__ __forceinline__ void xlane_pass(uint2 (&v)[8], bool left) {
 constexpr int kDppXor1 = 0xB1;  // quad_perm [1, 0, 3, 2]
 constexpr int kDppXor2 = 0x4E;  // quad_perm [2, 3, 0, 1]
 constexpr int kDppRev4 = 0x1B;  // quad_perm [3, 2, 1, 0]
+
+template <int TLOG>
+__global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_eu(4))) void sph_sort_tail_kernel(uint2* __restrict__ lookup) {
+  static_assert(TLOG >= 10 && TLOG <= 13, "eight entries per thread, 128..1024 threads");
+  constexpr uint32_t TILE = 1u << TLOG, NT = TILE / 8;
+  __shared__ uint2 lds[TILE + TILE / 32];
+  const uint32_t t = threadIdx.x;
+  uint2* tile = lookup + (size_t)blockIdx.x * TILE;
+  {  // strides TILE/2, TILE/4, TILE/8: group r = t, entries t + j * NT, straight from the lookup
+    uint2 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = tile[t + j * NT];
+    group_passes<3>(v);
+    const uint32_t a = padded(t);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) lds[a + pad_off<NT>(j)] = v[j];
+  }
+  __syncthreads();
+  lds_chunks<TLOG - 4>(lds, t);
+  {  // strides 8, 4, 2, 1: lane pair (2k, 2k + 1) holds the 16 entries [16k, 16k + 16)
+    const uint32_t a = padded(8u * t);
+    uint2 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = lds[a + i];
+    xlane_pass<kDppXor1, false>(v, (t & 1u) == 0u);  // stride 8: entry i of the left lane vs the right's
+    group_passes<3>(v);  // strides 4, 2, 1 inside the lane's eight
+    uint4* out = reinterpret_cast<uint4*>(tile + 8u * t);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[i] = make_uint4(v[2 * i].x, v[2 * i].y, v[2 * i + 1].x, v[2 * i + 1].y);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Static-network head launch: bin (wgsl:455-468) + every stage whose whole network fits one
+// tile (stages 0 .. TLOG-1), eight entries per thread.  Between stages a thread holds its eight
+// consecutive entries [8t, 8t + 8) in registers, and lane quads the 32 entries [32k, 32k + 32):
+// passes of stride 1, 2, 4 run inside a lane, strides 8 and 16 (and the flips of stages 3
+// and 4) across the quad with DPP moves, so stages 0-4 and the last five passes of every later
+// stage never touch LDS.  A later stage S writes its entries to LDS once, runs its flip chunk
+// (strides 2^S, 2^(S-1)) and its passes of strides 2^(S-2) .. 32 there in register chunks with
+// compile-time addresses, and reads its entries back.  The last stage stores them.  Same
+// compare-swaps in the same order as the reference's pass-per-dispatch schedule.
+// ---------------------------------------------------------------------------------------
+
 
 // Stages 0-2 (spans 2, 4, 8): inside the lane's eight consecutive entries.
 __device__ __forceinline__ void reg_stages012(uint2 (&v)[8]) {
@@ -1152,50 +1122,40 @@ __device__ __forceinline__ void bin_keys(const SortBin& bin, uint32_t base0, uin
   }
 }
 
-// TPW tiles per workgroup, one after the other, the next tile's bin inputs loaded before this
-// tile's stages (as in the tail launch).
-template <int TLOG, int TPW>
+template <int TLOG>
 __global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_eu(4))) void sph_sort_head_kernel(uint2* __restrict__ lookup, SortBin bin) {
   static_assert(TLOG >= 10 && TLOG <= 13, "eight entries per thread, 128..1024 threads");
   constexpr uint32_t TILE = 1u << TLOG, NT = TILE / 8;
   __shared__ uint2 lds[TILE + TILE / 32];
   const PaddedTile s{lds};
   const uint32_t t = threadIdx.x;
-  uint32_t base0 = blockIdx.x * TPW * TILE;
-  BinLoads in;
-  bin_load<NT>(lookup, bin, base0, t, in);
-#pragma unroll
-  for (int k = 0; k < TPW; ++k, base0 += TILE) {
-    BinLoads nxt;
-    if (k + 1 < TPW) bin_load<NT>(lookup, bin, base0 + TILE, t, nxt);
+  const uint32_t base0 = blockIdx.x * TILE;
+  {  // bin: every position (or pad entry) load first, then the keys
+    BinLoads in;
+    bin_load<NT>(lookup, bin, base0, t, in);
     bin_keys<NT>(bin, base0, t, in, s);
-    __syncthreads();
-    uint2 v[8];
-    const uint32_t a = padded(8u * t);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = lds[a + i];
-    reg_stages012(v);
-    xlane_pass<kDppXor1, true>(v, (t & 1u) == 0u);  // stage 3: flip G = 8 (lane pair), then 4, 2, 1
-    group_passes<3>(v);
-    xlane_pass<kDppRev4, true>(v, (t & 2u) == 0u);  // stage 4: flip G = 16 (lane quad), then 8 ... 1
-    reg_tail<false>(v, t);
-    // The bin's LDS image was read back by this lane only ([8t, 8t + 8)); its other entries were
-    // written by other waves before the barrier above, so stage 5's first write is safe.
-    head_stages<5, TLOG>(lds, t, v);
-    uint4* out = reinterpret_cast<uint4*>(lookup + base0 + 8u * t);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) out[i] = make_uint4(v[2 * i].x, v[2 * i].y, v[2 * i + 1].x, v[2 * i + 1].y);
-    if (k + 1 < TPW) {
-      in = nxt;
-      __syncthreads();  // every wave has read this tile's LDS image before the next bin writes
-    }
   }
+  __syncthreads();
+  uint2 v[8];
+  const uint32_t a = padded(8u * t);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = lds[a + i];
+  reg_stages012(v);
+  xlane_pass<kDppXor1, true>(v, (t & 1u) == 0u);  // stage 3: flip G = 8 (lane pair), then 4, 2, 1
+  group_passes<3>(v);
+  xlane_pass<kDppRev4, true>(v, (t & 2u) == 0u);  // stage 4: flip G = 16 (lane quad), then 8 ... 1
+  reg_tail<false>(v, t);
+  // The bin's LDS image was read back by this lane only ([8t, 8t + 8)); its other entries were
+  // written by other waves before the barrier above, so stage 5's first write is safe.
+  head_stages<5, TLOG>(lds, t, v);
+  uint4* out = reinterpret_cast<uint4*>(lookup + base0 + 8u * t);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) out[i] = make_uint4(v[2 * i].x, v[2 * i].y, v[2 * i + 1].x, v[2 * i + 1].y);
 }
 
 // ---------------------------------------------------------------------------------------
 // Static-network gathered-tile launch: all T >= 5 global passes of one stage (strides 2^s down to
-// the local tile 2^lg) in one launch, like sph_sort_stage_kernel below, with the schedule fixed at
-// compile time.  A workgroup gathers the residues r0 .. r0 + W - 1 (and their mirrors g - W - r0
+// the local tile 2^lg) in one launch, with the schedule fixed at compile time.  A workgroup gathers the residues r0 .. r0 + W - 1 (and their mirrors g - W - r0
 // .. g - 1 - r0) of every class j < 2^T: in tile order tau = 2W j + W c + k the stage's passes
 // are the tile's stage T + LW from its flip down to stride 2W.  The flip chunk (flip + the next
 // stride) loads its eight entries straight from the lookup, the last chunk stores straight to
@@ -1279,62 +1239,6 @@ __global__ __launch_bounds__(1u << (T + LW - 2)) __attribute__((amdgpu_waves_per
   gather_mid_chunks<TL - 3, LW + 1>(lds, t);  // strides TT/8 .. 2W, all but the last chunk
   constexpr int KL = T - 2 >= 3 ? 3 : T - 2;
   lds_chunk_out<LW + KL, KL>(lds, t, [&](uint32_t tau, uint2 e) { lookup[pos(tau)] = e; });
-}
-
-// All T global passes of one stage in one launch (T > 4 would take two or more register-fused
-// launches).  The passes have strides G = 2^s down to g = 2^lg (the LDS tile of the local
-// launches); as in sort_group, residue class r (positions r + j*g of a 2G block, j < 2^T)
-// together with its mirror class g-1-r is closed under them.  A workgroup takes 16
-// consecutive residues r0..r0+15 (r0 < g/2) and their mirrors: for each j one 128-B segment
-// of each class, 2^(T+5) entries in LDS.  In the tile's order tau = 32j + 16c + k (c = 1: the
-// mirror segment, ascending), which is the order of the original positions, the stage's flip
-// pass pairs tau with tile-1-tau and its stride g*2^m passes pair tau with tau + 32*2^m: the
-// passes of tile stage T+4 from step 0 down to group width 32.  Same network, same
-// compare-swaps, so the same result as T pass-per-dispatch launches.
-template <int KMAX, uint32_t CAP>
-__global__ __launch_bounds__(1024) void sph_sort_stage_kernel(uint2* __restrict__ lookup, uint32_t s,
-                                                              uint32_t lg, uint32_t T) {
-  __shared__ uint2 lds[CAP + CAP / 32];
-  const PaddedTile sm{lds};
-  const uint32_t tile = 32u << T;
-  const uint32_t g = 1u << lg;
-  const uint32_t rgs = lg - 5u;  // log2(residue groups of 16 in [0, g/2))
-  const uint32_t base = (blockIdx.x >> rgs) << (s + 1u);
-  const uint32_t r0 = (blockIdx.x & ((1u << rgs) - 1u)) << 4;
-  const auto pos = [&](uint32_t tau) {
-    const uint32_t j = tau >> 5, c = (tau >> 4) & 1u, k = tau & 15u;
-    return base + j * g + (c ? (g - 16u - r0 + k) : (r0 + k));
-  };
-  {  // 16-B aligned pairs, all of a lane's loads before its first LDS write (as in the local kernel)
-    uint4 v[kSortLd];
-#pragma unroll
-    for (uint32_t k = 0; k < kSortLd; ++k) {
-      const uint32_t q = 2u * threadIdx.x + k * 2u * blockDim.x;
-      if (q < tile) v[k] = *reinterpret_cast<const uint4*>(lookup + pos(q));
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < kSortLd; ++k) {
-      const uint32_t q = 2u * threadIdx.x + k * 2u * blockDim.x;
-      if (q < tile) {
-        sm[q] = make_uint2(v[k].x, v[k].y);
-        sm[q + 1u] = make_uint2(v[k].z, v[k].w);
-      }
-    }
-    for (uint32_t q = 2u * threadIdx.x + kSortLd * 2u * blockDim.x; q < tile; q += 2u * blockDim.x) {
-      const uint4 w = *reinterpret_cast<const uint4*>(lookup + pos(q));
-      sm[q] = make_uint2(w.x, w.y);
-      sm[q + 1u] = make_uint2(w.z, w.w);
-    }
-  }
-  __syncthreads();
-  for (uint32_t step = 0; step < T;) {
-    step += sort_chunk<KMAX>(sm, 0u, tile, T + 4u, step, threadIdx.x, blockDim.x, T - step);
-    __syncthreads();
-  }
-  for (uint32_t q = 2u * threadIdx.x; q < tile; q += 2u * blockDim.x) {
-    const uint2 a = sm[q], c = sm[q + 1u];
-    *reinterpret_cast<uint4*>(lookup + pos(q)) = make_uint4(a.x, a.y, c.x, c.y);
-  }
 }
 
 // calculate_spatial_lookup_offsets, compute_shader.wgsl:507-525: offsets[key] = the first
@@ -2260,27 +2164,12 @@ static hipError_t launch_sort_fused(uint2* lookup, uint32_t P, uint32_t G, bool 
   return hipGetLastError();
 }
 
-static hipError_t launch_sort_local(int kmax, bool bin, uint32_t tiles, uint32_t threads,
-                                    hipStream_t s, uint2* lookup, uint32_t tile, uint32_t lo,
-                                    uint32_t hi, uint32_t first, const SortBin& sb) {
-#define RPS_LOCAL(B, K)                                                                          \
-  if (tile > kSortTile)                                                                          \
-    hipLaunchKernelGGL((sph_sort_local_kernel<B, K, kSortTileMax>), dim3(tiles), dim3(threads), 0, \
-                       s, lookup, tile, lo, hi, first, sb, vec);                                 \
-  else                                                                                           \
-    hipLaunchKernelGGL((sph_sort_local_kernel<B, K>), dim3(tiles), dim3(threads), 0, s, lookup,  \
-                       tile, lo, hi, first, sb, vec)
-  // 16-B tile loads/stores, two entries per lane (8-B ones: 65 536 0.1157 -> 0.112 ms/frame,
-  // 2^19 -1.3 %); a one-entry tile (P == 1) takes the 8-B path.
-  const uint32_t vec = tile >= 2u ? 1u : 0u;
-  if (bin) {
-    if (kmax == 3) RPS_LOCAL(true, 3);
-    else RPS_LOCAL(true, 2);
-  } else {
-    if (kmax == 3) RPS_LOCAL(false, 3);
-    else RPS_LOCAL(false, 2);
-  }
-#undef RPS_LOCAL
+// Bin + the whole network of a lookup below 2048 entries (one tile of P entries, LDS passes in
+// register chunks of two).
+static hipError_t launch_sort_small(uint32_t threads, hipStream_t s, uint2* lookup, uint32_t tile,
+                                    uint32_t hi, const SortBin& sb) {
+  hipLaunchKernelGGL((sph_sort_local_kernel<true, 2>), dim3(1), dim3(threads), 0, s, lookup, tile, 0u, hi, 0u, sb,
+                     tile >= 2u ? 1u : 0u);
   return hipGetLastError();
 }
 
@@ -2293,7 +2182,6 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
   *passes = stages * (stages + 1u) / 2u;
   *launches = 0;
   const SortBin bin{b.cfg, b.st, b.offsets, b.n, b.lay.run2};
-  const SortBin nobin{nullptr, nullptr, nullptr, 0u, nullptr};
   if (stages == 0) {  // P == 1: nothing to sort, only bin
     hipLaunchKernelGGL((sph_sort_local_kernel<true, 1>), dim3(1), dim3(64), 0, s, b.lookup, 1u, 1u, 0u,
                        0u, bin, 0u);
@@ -2305,27 +2193,19 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
   // (DESIGN.md §5): 2048 up to P = 2^19, 4096 at 2^20, 8192 from 2^21.  A fixed 8192 above
   // 2^18 left half the CUs idle at 2^20 (0.429 -> 0.404 ms/frame) and 2^19 (0.294 -> 0.265).
   const uint32_t tile = std::min(P, std::min(kSortTile, std::max(2048u, P / 256u)));
-  // Passes per register chunk: 3 on 8192-entry tiles, 2 on smaller ones (measured at 65 536
-  // to 2^22 particles; 4 is slower everywhere: fewer waves per CU).
-  const int kmax = tile >= kSortTile ? 3 : 2;
   uint32_t tile_log = 0;
   while ((1u << tile_log) < tile) ++tile_log;
   const uint32_t tiles = P / tile;
   // Stages whose whole network fits one tile: one launch (with the bin pass).
   const uint32_t first_global_stage = tile_log;  // stage s has 2*2^s = 2^(s+1) span
-  const uint32_t lt = std::max(64u, std::min(1024u, tile >> kmax));
+  const uint32_t lt = std::max(64u, tile >> 2);  // P < 2048: two passes per register chunk
   hipError_t e = hipSuccess;
   switch (tile_log) {  // bin + stages [0, tile_log): the static-network head launch
-    case 13:
-      if (tiles >= 512u && RPS_HEAD_TPW == 2)
-        hipLaunchKernelGGL((sph_sort_head_kernel<13, 2>), dim3(tiles / 2), dim3(1024), 0, s, b.lookup, bin);
-      else
-        hipLaunchKernelGGL((sph_sort_head_kernel<13, 1>), dim3(tiles), dim3(1024), 0, s, b.lookup, bin);
-      break;
-    case 12: hipLaunchKernelGGL((sph_sort_head_kernel<12, 1>), dim3(tiles), dim3(512), 0, s, b.lookup, bin); break;
-    case 11: hipLaunchKernelGGL((sph_sort_head_kernel<11, 1>), dim3(tiles), dim3(256), 0, s, b.lookup, bin); break;
+    case 13: hipLaunchKernelGGL((sph_sort_head_kernel<13>), dim3(tiles), dim3(1024), 0, s, b.lookup, bin); break;
+    case 12: hipLaunchKernelGGL((sph_sort_head_kernel<12>), dim3(tiles), dim3(512), 0, s, b.lookup, bin); break;
+    case 11: hipLaunchKernelGGL((sph_sort_head_kernel<11>), dim3(tiles), dim3(256), 0, s, b.lookup, bin); break;
     default:  // P < 2048: one tile of P entries
-      e = launch_sort_local(kmax, true, tiles, lt, s, b.lookup, tile, 0u, first_global_stage - 1u, 0u, bin);
+      e = launch_sort_small(lt, s, b.lookup, tile, first_global_stage - 1u, bin);
       if (e != hipSuccess) return e;
   }
   e = hipGetLastError();
@@ -2338,17 +2218,9 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
     uint32_t T = 0;
     while (T <= stage && 2u * (1u << (stage - T)) > tile) ++T;
     uint32_t step = 0;
-    // Five global passes: one register-fused launch (32 entries per thread) once P gives it
-    // 2^17 threads; the gathered-tile launch below otherwise (2^22 frame 1.2352 -> 1.2248 ms;
-    // at 2^20 and 65 536 the fused launch is slower: 0.3852 -> 0.3882, 0.1157 -> 0.1213).
-    if (T == 5u && P >= (1u << 22)) {
-      e = launch_sort_fused<5>(b.lookup, P, 1u << stage, true, s);
-      ++*launches;
-      if (e != hipSuccess) return e;
-      step = T;
-    }
-    // Stages with five or more global passes run them all in one gathered-tile launch
-    // (sph_sort_stage_kernel).
+    // Stages with five to nine global passes run them all in one gathered-tile launch
+    // (sph_sort_gather_kernel; at T = 5 and 2^22 it also beats the 32-entry register-fused
+    // launch, 16.3 us: frame -4.5 us).
     if (step < T && T >= 5u && T <= 9u && tile_log >= 6u) {
       // Residue groups of 16 (of 8 at T = 9, so the gathered tile stays 8192 entries).
       const uint32_t lw = T == 9u ? 3u : 4u;
@@ -2381,18 +2253,11 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
       step += k;
     }
     if (step <= stage) {  // the stage's passes inside each tile: strides tile/2 .. 1
-      // Two tiles per workgroup once that still gives every CU a workgroup (P >= 2^22 here).
-      const bool two = tiles >= 512u && RPS_TAIL_TPW == 2;
       switch (tile_log) {
-        case 13:
-          if (two) hipLaunchKernelGGL((sph_sort_tail_kernel<13, 2>), dim3(tiles / 2), dim3(1024), 0, s, b.lookup);
-          else hipLaunchKernelGGL((sph_sort_tail_kernel<13, 1>), dim3(tiles), dim3(1024), 0, s, b.lookup);
-          break;
-        case 12: hipLaunchKernelGGL((sph_sort_tail_kernel<12, 1>), dim3(tiles), dim3(512), 0, s, b.lookup); break;
-        case 11: hipLaunchKernelGGL((sph_sort_tail_kernel<11, 1>), dim3(tiles), dim3(256), 0, s, b.lookup); break;
-        default:
-          e = launch_sort_local(kmax, false, tiles, lt, s, b.lookup, tile, stage, stage, step, nobin);
-          if (e != hipSuccess) return e;
+        case 13: hipLaunchKernelGGL((sph_sort_tail_kernel<13>), dim3(tiles), dim3(1024), 0, s, b.lookup); break;
+        case 12: hipLaunchKernelGGL((sph_sort_tail_kernel<12>), dim3(tiles), dim3(512), 0, s, b.lookup); break;
+        case 11: hipLaunchKernelGGL((sph_sort_tail_kernel<11>), dim3(tiles), dim3(256), 0, s, b.lookup); break;
+        default: return hipErrorInvalidValue;  // later stages exist only with 2048..8192-entry tiles
       }
       e = hipGetLastError();
       ++*launches;

@@ -78,16 +78,18 @@ def test_sph_config_validation(gpu):
         assert e.value.status == rps.RPS_ERR_UNSUPPORTED
 
 
-@pytest.mark.parametrize("n", [(1 << 20) + 5, 300000])
+@pytest.mark.parametrize("n", [(1 << 22) + 5, (1 << 20) + 5, 300000])
 def test_sph_grid_passes_large(gpu, orc, n):
-    """bin + bitonic + offsets at P = 2^21 / 2^19 (8192-entry LDS tiles, register-fused global
-    passes of up to 4 network steps) against the oracle's pass-per-dispatch network; passes
-    4-5 gated off (shader_delay) so only the integer passes run."""
+    """bin + bitonic + offsets at P = 2^23 / 2^21 / 2^19 against the oracle's pass-per-dispatch
+    network (OpenMP build, same network): 8192-entry head and tail tiles, register-fused global
+    passes, gathered-tile stages of 5-9 global passes, and at P = 2^23 the last stage's ten
+    global passes as register-fused launches with non-flip chunks; passes 4-5 gated off
+    (shader_delay) so only the integer passes run."""
     rps = gpu
     cfg = rps.default_particle_config(n, gravity=100.0)
     soa = _blob(n, 7, spread=300.0)
     ext = rps.make_ext(shader_delay=100)
-    st = orc.SphState(n)
+    st = orc.SphState(n, omp=True)
     ref = copy_soa(soa)
     with rps.Context(n, rps.MODE_SPH) as ctx:
         ctx.set_config(cfg, ext)
