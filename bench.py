@@ -22,7 +22,6 @@ Prints ONE JSON line on rank 0 (fields: see the contract in DESIGN.md §6).
 import argparse
 import json
 import os
-import statistics
 import sys
 import time
 
@@ -55,9 +54,6 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=1 << 22, help="CPU-baseline particles")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=0x5EED)
-    ap.add_argument("--profile-every", type=int, default=0,
-                    help="bracket every k-th kernel launch with HIP events (roofline.achieved); 0: every "
-                         "launch up to 64 timed steps, every (steps // 64)-th beyond; -1: off")
     ap.add_argument("--allpairs-n", type=int, default=1 << 22,
                     help="global particles of the all-pairs N-body side measurement (0: skip)")
     ap.add_argument("--allpairs-steps", type=int, default=2)
@@ -521,23 +517,19 @@ def main():
 
     d.sync_device()
     d.barrier()
-    period = args.profile_every if args.profile_every else max(1, args.steps // 64)
-    ctx.set_profiling(max(0, period))
     t0 = time.perf_counter()
-    ctx.step(args.steps)
+    # The K steps between one pair of HIP events on the context stream (rps_time_steps): the
+    # average launch is their span / K.  Launches run back to back (no event between them:
+    # round 2 bracketed launches one by one, and each event pair left a ~12-us idle gap on the
+    # GPU); the span includes the stats steps that fall in the region.
+    gpu_ms = ctx.time_steps(args.steps)
     ctx.sync()
     d.sync_device()
     t1 = time.perf_counter()
     d.barrier()
     elapsed = d.max(t1 - t0)
-    # Per-launch durations of the bracketed launches (HIP events on the context stream); the
-    # roofline uses their median, so a launch with a late event or a slow first dispatch does
-    # not set it.
-    times = ctx.kernel_times() if period > 0 else []
-    launches = len(times)
-    kern_med = d.max(statistics.median(times)) if times else float("nan")
-    kern_mean = d.max(statistics.mean(times)) if times else float("nan")
-    kern_ms = kern_med
+    kern_ms = d.max(gpu_ms / args.steps)
+    launches = args.steps
     moved_per_launch, _ = ctx.step_cost()  # bytes the kernel moves: 32.03 B per particle
     algo_per_launch = ALGO_BYTES_PER_PARTICLE * n
     export = export_side(ctx, n, args.export_reps) if args.export_reps > 0 and hasattr(ctx, "stream_ptr") else None
@@ -573,8 +565,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS,
                      "traffic": traffic, "kernel": "stream_step_kernel<euler,lifetime>",
-                     "median_kernel_ms": kern_med, "avg_kernel_ms": kern_mean, "launches": launches,
-                     "profile_every": period,
+                     "avg_kernel_ms": kern_ms, "launches": launches,
+                     "timing": "one HIP event pair on the context stream around the K timed launches",
                      "algorithmic_bytes_per_launch": algo_per_launch,
                      "moved_bytes_per_launch": moved_per_launch, "moved_gbps": moved_gbps,
                      "moved_frac": moved_gbps / HBM_PEAK_GBPS,

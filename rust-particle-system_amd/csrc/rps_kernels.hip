@@ -886,13 +886,13 @@ __device__ __forceinline__ constexpr uint32_t pad_off(uint32_t j) {
 }
 __device__ __forceinline__ uint32_t padded(uint32_t e) { return e + (e >> 5); }
 
-// One LDS chunk: passes of strides 2^LG down to 2^(LG-K+1), non-flip, 2^(3-K) groups per thread
-// (eight entries), thread t taking groups t * 2^(3-K) + i.
-template <int LG, int K>
+// One LDS chunk: passes of strides 2^LG down to 2^(LG-K+1), non-flip, 2^(LE-K) groups per thread
+// (2^LE entries, eight by default), thread t taking groups t * 2^(LE-K) + i.
+template <int LG, int K, int LE = 3>
 __device__ __forceinline__ void lds_chunk(uint2* lds, uint32_t t) {
   constexpr int LGG = LG - K + 1;
   constexpr uint32_t g = 1u << LGG;
-  constexpr int NG = 1 << (3 - K);
+  constexpr int NG = 1 << (LE - K);
 #pragma unroll
   for (int i = 0; i < NG; ++i) {
     const uint32_t q = t * NG + i;
@@ -1163,11 +1163,11 @@ __global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_e
 // ---------------------------------------------------------------------------------------
 
 // A non-flip register chunk read from LDS, stored through `store(tau, entry)`.
-template <int LG, int K, class Store>
+template <int LG, int K, int LE, class Store>
 __device__ __forceinline__ void lds_chunk_out(const uint2* lds, uint32_t t, Store&& store) {
   constexpr int LGG = LG - K + 1;
   constexpr uint32_t g = 1u << LGG;
-  constexpr int NG = 1 << (3 - K);
+  constexpr int NG = 1 << (LE - K);
 #pragma unroll
   for (int i = 0; i < NG; ++i) {
     const uint32_t q = t * NG + i;
@@ -1182,25 +1182,30 @@ __device__ __forceinline__ void lds_chunk_out(const uint2* lds, uint32_t t, Stor
   }
 }
 
-// Non-flip strides 2^LG down to 2^LO in LDS chunks of up to three passes, the lowest chunk
-// (up to three passes) left for lds_chunk_out.
-template <int LG, int LO>
+// Non-flip strides 2^LG down to 2^LO in LDS chunks of up to LE passes, the lowest chunk (up to
+// LE passes) left for lds_chunk_out.
+template <int LG, int LO, int LE>
 __device__ __forceinline__ void gather_mid_chunks(uint2* lds, uint32_t t) {
   constexpr int left = LG - LO + 1;  // passes from 2^LG down to 2^LO
-  if constexpr (left > 3) {
-    constexpr int K = (left - 3) % 3 == 0 ? 3 : (left - 3) % 3;
-    lds_chunk<LG, K>(lds, t);
+  if constexpr (left > LE) {
+    constexpr int K = (left - LE) % LE == 0 ? LE : (left - LE) % LE;
+    lds_chunk<LG, K, LE>(lds, t);
     __syncthreads();
-    gather_mid_chunks<LG - K, LO>(lds, t);
+    gather_mid_chunks<LG - K, LO, LE>(lds, t);
   }
 }
 
-template <int T, int LW>
-__global__ __launch_bounds__(1u << (T + LW - 2)) __attribute__((amdgpu_waves_per_eu(4))) void sph_sort_gather_kernel(
+// 2^LE entries per thread: 8, or 16 for the nine-pass stage, whose 16-residue tile of 16 384
+// entries would otherwise need 2048 threads (residue groups of 8 instead split every 128-B line
+// between two workgroups: twice the L2 reads, 1.5x the HBM bytes, 22.0 us).
+template <int T, int LW, int LE>
+__global__ __launch_bounds__(1u << (T + LW + 1 - LE)) __attribute__((amdgpu_waves_per_eu(4))) void sph_sort_gather_kernel(
     uint2* __restrict__ lookup, uint32_t s, uint32_t lg) {
-  static_assert(T >= 5 && T + LW + 1 <= 13, "eight entries per thread, at most 1024 threads");
+  static_assert(T >= 5 && T + LW + 1 - LE <= 10, "at most 1024 threads");
   constexpr int TL = T + LW + 1;  // log2 of the gathered tile
-  constexpr uint32_t TT = 1u << TL, W = 1u << LW, gp = TT / 4;
+  constexpr int M = 1 << (LE - 1);  // entries per class in the flip chunk
+  constexpr uint32_t TT = 1u << TL, W = 1u << LW, gp = TT >> (LE - 1);  // gp: the flip chunk's stride g'
+  constexpr int KF = LE - 1;  // passes of the flip chunk (the flip and KF - 1 strides)
   __shared__ uint2 lds[TT + TT / 32];
   const uint32_t g = 1u << lg;
   const uint32_t rgs = lg - LW - 1u;  // log2(residue groups of W in [0, g/2))
@@ -1211,34 +1216,36 @@ __global__ __launch_bounds__(1u << (T + LW - 2)) __attribute__((amdgpu_waves_per
     return base + j * g + (c ? (g - W - r0 + k) : (r0 + k));
   };
   const uint32_t t = threadIdx.x;
-  {  // the flip (G' = TT/2) and stride TT/4 on class t and its mirror gp - 1 - t, from memory
-    uint2 v[8];
+  {  // the flip (G' = TT/2) and strides TT/4 .. gp on class t and its mirror gp - 1 - t, from memory
+    uint2 v[2 * M];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < M; ++j) {
       v[j] = lookup[pos(t + j * gp)];
-      v[4 + j] = lookup[pos(gp - 1u - t + j * gp)];
+      v[M + j] = lookup[pos(gp - 1u - t + j * gp)];
     }
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      cas(v[j], v[7 - j]);
-      cas(v[4 + j], v[3 - j]);
+    for (int j = 0; j < M / 2; ++j) {  // flip: position t + j*gp pairs with (gp-1-t) + (M-1-j)*gp
+      cas(v[j], v[2 * M - 1 - j]);
+      cas(v[M + j], v[M - 1 - j]);
     }
 #pragma unroll
-    for (int c = 0; c < 8; c += 4) {
-      cas(v[c], v[c + 1]);
-      cas(v[c + 2], v[c + 3]);
-    }
+    for (int m = KF - 2; m >= 0; --m)  // strides gp * 2^m inside each class
+#pragma unroll
+      for (int c = 0; c < 2 * M; c += M)
+#pragma unroll
+        for (int j = 0; j < M; ++j)
+          if (!(j & (1 << m))) cas(v[c + j], v[c + j + (1 << m)]);
     const uint32_t a = padded(t), b = padded(gp - 1u - t);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < M; ++j) {
       lds[a + pad_off<gp>(j)] = v[j];
-      lds[b + pad_off<gp>(j)] = v[4 + j];
+      lds[b + pad_off<gp>(j)] = v[M + j];
     }
   }
   __syncthreads();
-  gather_mid_chunks<TL - 3, LW + 1>(lds, t);  // strides TT/8 .. 2W, all but the last chunk
-  constexpr int KL = T - 2 >= 3 ? 3 : T - 2;
-  lds_chunk_out<LW + KL, KL>(lds, t, [&](uint32_t tau, uint2 e) { lookup[pos(tau)] = e; });
+  gather_mid_chunks<TL - LE, LW + 1, LE>(lds, t);  // strides gp/2 .. 2W, all but the last chunk
+  constexpr int KL = T + 1 - LE >= LE ? LE : T + 1 - LE;
+  lds_chunk_out<LW + KL, KL, LE>(lds, t, [&](uint32_t tau, uint2 e) { lookup[pos(tau)] = e; });
 }
 
 // calculate_spatial_lookup_offsets, compute_shader.wgsl:507-525: offsets[key] = the first
@@ -2222,16 +2229,15 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
     // (sph_sort_gather_kernel; at T = 5 and 2^22 it also beats the 32-entry register-fused
     // launch, 16.3 us: frame -4.5 us).
     if (step < T && T >= 5u && T <= 9u && tile_log >= 6u) {
-      // Residue groups of 16 (of 8 at T = 9, so the gathered tile stays 8192 entries).
-      const uint32_t lw = T == 9u ? 3u : 4u;
-      const uint32_t blocks = (P >> (stage + 1u)) << (tile_log - lw - 1u);
-      const uint32_t threads = (2u << (T + lw)) / 8u;
+      // Residue groups of 16 (whole 128-B lines); eight entries per thread, sixteen at T = 9.
+      const uint32_t blocks = (P >> (stage + 1u)) << (tile_log - 5u);
+      const uint32_t threads = T == 9u ? 1024u : (32u << T) / 8u;
       switch (T) {
-        case 5: hipLaunchKernelGGL((sph_sort_gather_kernel<5, 4>), dim3(blocks), dim3(threads), 0, s, b.lookup, stage, tile_log); break;
-        case 6: hipLaunchKernelGGL((sph_sort_gather_kernel<6, 4>), dim3(blocks), dim3(threads), 0, s, b.lookup, stage, tile_log); break;
-        case 7: hipLaunchKernelGGL((sph_sort_gather_kernel<7, 4>), dim3(blocks), dim3(threads), 0, s, b.lookup, stage, tile_log); break;
-        case 8: hipLaunchKernelGGL((sph_sort_gather_kernel<8, 4>), dim3(blocks), dim3(threads), 0, s, b.lookup, stage, tile_log); break;
-        default: hipLaunchKernelGGL((sph_sort_gather_kernel<9, 3>), dim3(blocks), dim3(threads), 0, s, b.lookup, stage, tile_log); break;
+        case 5: hipLaunchKernelGGL((sph_sort_gather_kernel<5, 4, 3>), dim3(blocks), dim3(threads), 0, s, b.lookup, stage, tile_log); break;
+        case 6: hipLaunchKernelGGL((sph_sort_gather_kernel<6, 4, 3>), dim3(blocks), dim3(threads), 0, s, b.lookup, stage, tile_log); break;
+        case 7: hipLaunchKernelGGL((sph_sort_gather_kernel<7, 4, 3>), dim3(blocks), dim3(threads), 0, s, b.lookup, stage, tile_log); break;
+        case 8: hipLaunchKernelGGL((sph_sort_gather_kernel<8, 4, 3>), dim3(blocks), dim3(threads), 0, s, b.lookup, stage, tile_log); break;
+        default: hipLaunchKernelGGL((sph_sort_gather_kernel<9, 4, 4>), dim3(blocks), dim3(threads), 0, s, b.lookup, stage, tile_log); break;
       }
       e = hipGetLastError();
       ++*launches;

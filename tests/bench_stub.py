@@ -63,6 +63,10 @@ class Context:
     def sync(self):
         pass
 
+    def time_steps(self, nsteps):
+        self.step(nsteps)
+        return 0.5 * nsteps
+
     def set_profiling(self, period=1):
         pass
 

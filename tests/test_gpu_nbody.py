@@ -104,6 +104,27 @@ def test_nbody_shard_without_comm_is_rejected(gpu):
         assert e.value.status == rps.RPS_ERR_COMM
 
 
+def test_nbody_kernel_clock(gpu):
+    """rps_get_kernel_clock: refused before a profiled force launch; afterwards the median over
+    the launch's workgroups of their in-kernel s_memtime / s_memrealtime stamps, a plausible
+    shader clock (MI355X: at most 2400 MHz), from every workgroup of the launch."""
+    rps = gpu
+    n = 1 << 16
+    with rps.Context(n, rps.MODE_NBODY) as ctx:
+        ctx.set_config(config_c1(rps, n), rps.make_ext(nbody_strength=10.0, nbody_softening=1.0, shader_delay=0))
+        ctx.init_scatter(3)
+        ctx.step(1)
+        with pytest.raises(rps.RpsError):
+            ctx.kernel_clock()
+        ctx.set_profiling(1)
+        ctx.step(2)
+        mhz, wgs = ctx.kernel_clock()
+        ms, launches = ctx.kernel_time()
+    assert launches == 2 and ms > 0
+    assert 300.0 < mhz < 2600.0, mhz
+    assert wgs == 32 * 64  # 32 target blocks x 64 source splits (kNbodyMaxSplits), every one stamped
+
+
 def test_nbody_single_rank_comm(gpu, orc):
     """RCCL path with one rank exercises rps_comm_init + the all-gather call."""
     rps = gpu

@@ -296,6 +296,13 @@ def test_profiling_counts_dominant_kernel(gpu):
         amt, unit = ctx.step_cost()
         assert unit == "bytes" and amt == (32 + 2 / 64) * n  # x, y, vx, vy r+w + the groups' [next] read
         assert ctx.time_steps(3) > 0
+        ctx.set_profiling(2)  # every 2nd launch: 3 of 6 (launch-by-launch view)
+        ctx.step(6)
+        times = ctx.kernel_times()
+        assert len(times) == 3 and all(t > 0 for t in times)
+        assert ctx.kernel_times() == []  # a new collection
+        with pytest.raises(rps.RpsError):
+            ctx.kernel_clock()  # N-body mode only
 
 
 @pytest.mark.parametrize("fuse,n,steps", [(4, 1 << 20, 13), (16, 65539, 40), (7, 5, 9)])

@@ -50,10 +50,10 @@ def xlane(v, partner, rev, left):
     v[sw] = p[sw]
 
 
-def lds_chunk(lds, nt, LG, K):
+def lds_chunk(lds, nt, LG, K, LE=3):
     LGG = LG - K + 1
     g = 1 << LGG
-    NG = 1 << (3 - K)
+    NG = 1 << (LE - K)
     for i in range(NG):
         q = np.arange(nt) * NG + i
         e0 = ((q >> LGG) << (LG + 1)) + (q & (g - 1))
@@ -185,13 +185,15 @@ def ref_passes(a, stage, steps):
     return a
 
 
-def gather_stage(a, s, lg, T, LW):
-    """sph_sort_gather_kernel<T, LW> over every workgroup (rps_kernels.hip)."""
+def gather_stage(a, s, lg, T, LW, LE=3):
+    """sph_sort_gather_kernel<T, LW, LE> over every workgroup (rps_kernels.hip)."""
     a = a.copy()
     P = len(a)
     TL = T + LW + 1
-    TT, W, gp = 1 << TL, 1 << LW, 1 << (TL - 2)
-    nt = TT // 8
+    TT, W = 1 << TL, 1 << LW
+    gp = TT >> (LE - 1)
+    M = 1 << (LE - 1)
+    nt = TT >> LE
     g = 1 << lg
     rgs = lg - LW - 1
     blocks = (P >> (s + 1)) << rgs
@@ -203,36 +205,39 @@ def gather_stage(a, s, lg, T, LW):
         j, c, k = tau >> (LW + 1), (tau >> LW) & 1, tau & (W - 1)
         pos = base + j * g + np.where(c == 1, g - W - r0 + k, r0 + k)
         lds = a[pos].copy()
-        ia = t[:, None] + np.arange(4)[None, :] * gp
-        ib = (gp - 1 - t)[:, None] + np.arange(4)[None, :] * gp
+        ia = t[:, None] + np.arange(M)[None, :] * gp
+        ib = (gp - 1 - t)[:, None] + np.arange(M)[None, :] * gp
         v = np.concatenate([lds[ia], lds[ib]], 1)
-        for jj in range(2):
-            cas(v, jj, 7 - jj)
-            cas(v, 4 + jj, 3 - jj)
-        for cc in (0, 4):
-            cas(v, cc, cc + 1)
-            cas(v, cc + 2, cc + 3)
-        lds[ia], lds[ib] = v[:, :4], v[:, 4:]
-        LG, LO = TL - 3, LW + 1
-        while LG - LO + 1 > 3:
+        for jj in range(M // 2):
+            cas(v, jj, 2 * M - 1 - jj)
+            cas(v, M + jj, M - 1 - jj)
+        for m in range(LE - 3, -1, -1):
+            for cc in (0, M):
+                for jj in range(M):
+                    if not jj & (1 << m):
+                        cas(v, cc + jj, cc + jj + (1 << m))
+        lds[ia], lds[ib] = v[:, :M], v[:, M:]
+        LG, LO = TL - LE, LW + 1
+        while LG - LO + 1 > LE:
             left = LG - LO + 1
-            K = 3 if (left - 3) % 3 == 0 else (left - 3) % 3
-            lds_chunk(lds, nt, LG, K)
+            K = LE if (left - LE) % LE == 0 else (left - LE) % LE
+            lds_chunk(lds, nt, LG, K, LE)
             LG -= K
-        lds_chunk(lds, nt, LG, LG - LO + 1)  # the last chunk (stored to memory by the kernel)
+        lds_chunk(lds, nt, LG, LG - LO + 1, LE)  # the last chunk (stored to memory by the kernel)
         a[pos] = lds
     return a
 
 
-@pytest.mark.parametrize("T,LW", [(5, 4), (6, 4), (7, 4), (8, 4), (9, 3)])
+@pytest.mark.parametrize("T,LW,LE", [(5, 4, 3), (6, 4, 3), (7, 4, 3), (8, 4, 3), (9, 4, 4), (9, 3, 3)])
 @pytest.mark.parametrize("kmax", [5, 1 << 20])
-def test_gather_stage_schedule_equals_network(T, LW, kmax):
+def test_gather_stage_schedule_equals_network(T, LW, LE, kmax):
     """A stage's T global passes (local tiles of 2^lg entries, stage s = lg + T - 1) as the
-    gathered-tile launch runs them, against the reference's passes of that stage on the array."""
+    gathered-tile launch runs them (2^LE entries per thread), against the reference's passes of
+    that stage on the array."""
     lg = LW + 2
     s = lg + T - 1
     P = 1 << (s + 2)
-    g = np.random.default_rng(T * 13 + LW + (kmax & 7))
+    g = np.random.default_rng(T * 13 + LW + LE + (kmax & 7))
     keys = g.integers(0, kmax, P)
     a = np.stack([keys, np.arange(P)], 1).astype(np.int64)
-    np.testing.assert_array_equal(gather_stage(a, s, lg, T, LW), ref_passes(a, s, range(T)))
+    np.testing.assert_array_equal(gather_stage(a, s, lg, T, LW, LE), ref_passes(a, s, range(T)))

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round 3 measurement call: the default bench line, the driver's command twice, a kernel trace
+# of the default bench (profiles/), the stream PMC passes, and a kernel trace of SPH frames.
+# Each GPU step has its own time limit; the first failure ends the script.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out/r03m
+export TMPDIR=/tmp
+O=gpurun_out/r03m
+step() { local name=$1 t=$2; shift 2; echo "== $name"; timeout -k 10 "$t" "$@" > $O/$name.out 2> $O/$name.err || { echo "$name failed rc=$?"; tail -20 $O/$name.err; exit 1; }; }
+step bench_default 400 python3 bench.py
+step drv20_a 240 python3 bench.py --gpus 1 --steps 20 --warmup 5
+step drv20_b 240 python3 bench.py --gpus 1 --steps 20 --warmup 5
+step prof_bench 500 rocprofv3 --kernel-trace --stats -d $O/prof_bench -o run --output-format csv -- python3 bench.py
+step pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 40 --warmup 10 --no-cpu-baseline --allpairs-n 0 --sph-n 0 --no-configs --export-reps 0
+step pmc_write 120 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- python3 bench.py --steps 40 --warmup 10 --no-cpu-baseline --allpairs-n 0 --sph-n 0 --no-configs --export-reps 0
+step prof_sph 300 rocprofv3 --kernel-trace --stats -d $O/prof_sph -o run --output-format csv -- python3 tools/sph_frames.py 4194304 60
+for f in bench_default drv20_a drv20_b; do python3 -c "import json;d=json.load(open('$O/$f.out'));r=d['roofline'];print('$f',d['ms_per_step'],r['avg_kernel_ms'],r['frac'],r['moved_frac'],d.get('sph',{}).get('ms_per_frame'),d.get('allpairs',{}).get('roofline',{}).get('frac_at_sustained_clock'))"; done
