@@ -1,6 +1,6 @@
 """Turn rocprofv3 output under gpurun_out/ into the committed evidence under profiles/.
 
-  python tools/collect_profiles.py <round-tag>
+  python tools/collect_profiles.py <round-tag> [gpurun_out subdirectory]
 
 reads  gpurun_out/prof_trace/run_kernel_{stats,trace}.csv   (--kernel-trace --stats run of
        the bench command) and gpurun_out/pmc_{fetch,write}/run_counter_collection.csv (two
@@ -27,10 +27,12 @@ WORKLOAD = "C3-1e8-4att-drag-respawn-euler"
 DOMINANT = "stream_step_kernel<false, true, false, 3>"
 
 
-def main(tag):
+def main(tag, sub=""):
     os.makedirs(PROF, exist_ok=True)
-    stats = os.path.join(OUT, "prof_trace", "run_kernel_stats.csv")
-    trace = os.path.join(OUT, "prof_trace", "run_kernel_trace.csv")
+    base = os.path.join(OUT, sub)
+    trace_dir = "prof_bench" if sub else "prof_trace"
+    stats = os.path.join(base, trace_dir, "run_kernel_stats.csv")
+    trace = os.path.join(base, trace_dir, "run_kernel_trace.csv")
     summary = {}
     if os.path.exists(stats):
         shutil.copy(stats, os.path.join(PROF, f"{tag}_kernel_stats.csv"))
@@ -43,7 +45,7 @@ def main(tag):
                           "min_us": min(v), "max_us": max(v)}
     pmc = defaultdict(dict)
     for name, counter in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")):
-        f = os.path.join(OUT, name, "run_counter_collection.csv")
+        f = os.path.join(base, name, "run_counter_collection.csv")
         if not os.path.exists(f):
             continue
         vals = defaultdict(list)
@@ -76,4 +78,4 @@ def main(tag):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
+    main(sys.argv[1] if len(sys.argv) > 1 else "r01", sys.argv[2] if len(sys.argv) > 2 else "")
