@@ -50,92 +50,123 @@ def xlane(v, partner, rev, left):
     v[sw] = p[sw]
 
 
+def chunk_groups(nt, LNG):
+    """chunk_group<LNG>: a wave's 64 * 2^LNG groups, consecutive lanes on consecutive groups."""
+    t = np.arange(nt)
+    return [((t >> 6) << (6 + LNG)) + (i << 6) + (t & 63) for i in range(1 << LNG)]
+
+
 def lds_chunk(lds, nt, LG, K, LE=3):
     LGG = LG - K + 1
     g = 1 << LGG
-    NG = 1 << (LE - K)
-    for i in range(NG):
-        q = np.arange(nt) * NG + i
+    seen = []
+    for q in chunk_groups(nt, LE - K):
+        seen.append(q)
         e0 = ((q >> LGG) << (LG + 1)) + (q & (g - 1))
         idx = e0[:, None] + np.arange(1 << K)[None, :] * g
         v = lds[idx].copy()
         group_passes(v, K)
         lds[idx] = v
+    q = np.concatenate(seen)
+    assert len(q) == len(np.unique(q)) == len(lds) >> K  # every group exactly once
+
+
+def reg_tail(v, t, S):
+    """Strides 32 (xor-2 lanes), 16 (xor-1 lanes) when the stage has them, then 8 .. 1 in-lane."""
+    if S >= 8:
+        xlane(v, t ^ 2, False, (t & 2) == 0)
+    if S >= 7:
+        xlane(v, t ^ 1, False, (t & 1) == 0)
+    group_passes(v, 4)
+
+
+def mid_chunks(lds, nt, LG):
+    """lds_mid_chunks: non-flip strides 2^LG down to 64, up to four passes per chunk."""
+    while LG >= 6:
+        K = min(4, LG - 5)
+        lds_chunk(lds, nt, LG, K, 4)
+        LG -= K
 
 
 def tail(tile, TLOG):
-    nt = 1 << (TLOG - 3)
+    nt = 1 << (TLOG - 4)
     t = np.arange(nt)
-    v = tile[t[:, None] + np.arange(8)[None, :] * nt].copy()
-    group_passes(v, 3)
+    ia = t[:, None] + np.arange(16)[None, :] * nt
+    v = tile[ia].copy()
+    group_passes(v, 4)
     lds = np.zeros_like(tile)
-    lds[t[:, None] + np.arange(8)[None, :] * nt] = v
-    LG = TLOG - 4
-    while LG >= 4:
-        K = 3 if LG - 3 >= 3 else LG - 3
-        lds_chunk(lds, nt, LG, K)
-        LG -= K
-    v = lds[8 * t[:, None] + np.arange(8)[None, :]].copy()
-    xlane(v, t ^ 1, False, (t & 1) == 0)
-    group_passes(v, 3)
+    lds[ia] = v
+    mid_chunks(lds, nt, TLOG - 5)
+    v = lds[16 * t[:, None] + np.arange(16)[None, :]].copy()
+    reg_tail(v, t, 8)
     return v.reshape(-1, 2)
+
+
+def lane_stage(v, S):
+    B = 1 << (S + 1)
+    for b in range(0, 16, B):
+        for r in range(B // 2):
+            cas(v, b + r, b + B - 1 - r)
+    for m in range(S - 1, -1, -1):
+        for j in range(16):
+            if not j & (1 << m):
+                cas(v, j, j + (1 << m))
 
 
 def head(tile, TLOG):
-    nt = 1 << (TLOG - 3)
+    nt = 1 << (TLOG - 4)
     t = np.arange(nt)
-    v = tile.reshape(nt, 8, 2).copy()
-    for i in range(0, 8, 2):
-        cas(v, i, i + 1)
-    for b in (0, 4):
-        cas(v, b, b + 3)
-        cas(v, b + 1, b + 2)
-    for i in range(0, 8, 2):
-        cas(v, i, i + 1)
-    for j in range(4):
-        cas(v, j, 7 - j)
-    for b in (0, 4):
-        cas(v, b, b + 2)
-        cas(v, b + 1, b + 3)
-    for i in range(0, 8, 2):
-        cas(v, i, i + 1)
-    xlane(v, t ^ 1, True, (t & 1) == 0)  # stage 3
-    group_passes(v, 3)
-    xlane(v, t ^ 3, True, (t & 2) == 0)  # stage 4
+    v = tile.reshape(nt, 16, 2).copy()
+    for S in range(4):
+        lane_stage(v, S)
+    xlane(v, t ^ 1, True, (t & 1) == 0)  # stage 4: flip across the lane pair
+    group_passes(v, 4)
+    xlane(v, t ^ 3, True, (t & 2) == 0)  # stage 5: flip across the lane quad
     xlane(v, t ^ 1, False, (t & 1) == 0)
-    group_passes(v, 3)
+    group_passes(v, 4)
     lds = np.zeros_like(tile)
-    own = 8 * t[:, None] + np.arange(8)[None, :]
-    for S in range(5, TLOG):
+    own = 16 * t[:, None] + np.arange(16)[None, :]
+    for S in range(6, TLOG):
         lds[own] = v
-        g = 1 << (S - 1)
-        LP = S - 2
+        g = 1 << (S - 2)
+        LP = S - 3
         base = (t >> LP) << (S + 1)
         r = t & ((1 << LP) - 1)
-        ia = base[:, None] + r[:, None] + np.arange(4)[None, :] * g
-        ib = base[:, None] + (g - 1 - r)[:, None] + np.arange(4)[None, :] * g
+        ia = base[:, None] + r[:, None] + np.arange(8)[None, :] * g
+        ib = base[:, None] + (g - 1 - r)[:, None] + np.arange(8)[None, :] * g
         w = np.concatenate([lds[ia], lds[ib]], 1)
-        for j in range(2):
-            cas(w, j, 7 - j)
-            cas(w, 4 + j, 3 - j)
-        for c in (0, 4):
-            cas(w, c, c + 1)
-            cas(w, c + 2, c + 3)
-        lds[ia], lds[ib] = w[:, :4], w[:, 4:]
-        LG = S - 2
-        while LG >= 5:
-            K = 3 if LG - 4 >= 3 else LG - 4
-            lds_chunk(lds, nt, LG, K)
-            LG -= K
+        for j in range(4):
+            cas(w, j, 15 - j)
+            cas(w, 8 + j, 7 - j)
+        for c in (0, 8):
+            for m in (1, 0):
+                for j in range(8):
+                    if not j & (1 << m):
+                        cas(w, c + j, c + j + (1 << m))
+        lds[ia], lds[ib] = w[:, :8], w[:, 8:]
+        mid_chunks(lds, nt, S - 3)
         v = lds[own].copy()
-        if S >= 6:
-            xlane(v, t ^ 2, False, (t & 2) == 0)
-        xlane(v, t ^ 1, False, (t & 1) == 0)
-        group_passes(v, 3)
+        reg_tail(v, t, S)
     return v.reshape(-1, 2)
 
 
-@pytest.mark.parametrize("TLOG", [11, 12, 13])
+def store_sixteen(v, t):
+    """The quad transposition of store_sixteen: where each lane's sixteen entries land."""
+    nt = len(t)
+    out = np.full((nt * 16, 2), -1, dtype=v.dtype)
+    for h in (0, 1):
+        pairs = v[:, 8 * h:8 * h + 8].reshape(nt, 4, 2, 2)  # [lane, pair, entry, (key, payload)]
+        # after two quad_swap_bit steps lane l's pair m is lane m's pair l (within the quad)
+        q, l = t >> 2, t & 3
+        for m in range(4):
+            src = pairs[4 * q + m, l]  # lane (4q + m)'s pair l
+            dst = 64 * q + 16 * m + 8 * h + 2 * l
+            out[dst] = src[:, 0]
+            out[dst + 1] = src[:, 1]
+    return out
+
+
+@pytest.mark.parametrize("TLOG", [10, 11, 12, 13])
 @pytest.mark.parametrize("kmax", [7, 1 << 20])
 def test_head_schedule_equals_network(TLOG, kmax):
     g = np.random.default_rng(TLOG * 7 + (kmax & 3))
@@ -144,7 +175,7 @@ def test_head_schedule_equals_network(TLOG, kmax):
     np.testing.assert_array_equal(head(tile, TLOG), ref_network(keys, TLOG))
 
 
-@pytest.mark.parametrize("TLOG", [11, 12, 13])
+@pytest.mark.parametrize("TLOG", [10, 11, 12, 13])
 @pytest.mark.parametrize("kmax", [7, 1 << 20])
 def test_tail_schedule_equals_network(TLOG, kmax):
     """A later stage s's passes inside one tile: strides 2^(TLOG-1) .. 1, non-flip (the tile
@@ -166,6 +197,15 @@ def test_tail_schedule_equals_network(TLOG, kmax):
         l, r = a[left[sw]].copy(), a[right[sw]].copy()
         a[left[sw]], a[right[sw]] = r, l
     np.testing.assert_array_equal(tail(tile, TLOG), a)
+
+
+def test_store_sixteen_places_each_lane_contiguously():
+    """store_sixteen writes lane t's sixteen entries to [16t, 16t + 16), each store instruction
+    (fixed m, h) covering one whole 64-B segment per lane quad."""
+    nt = 64
+    t = np.arange(nt)
+    v = np.stack([np.arange(nt * 16), np.arange(nt * 16)], 1).reshape(nt, 16, 2)
+    np.testing.assert_array_equal(store_sixteen(v, t), v.reshape(-1, 2))
 
 
 def ref_passes(a, stage, steps):
