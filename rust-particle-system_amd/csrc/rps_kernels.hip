@@ -860,12 +860,68 @@ __global__ __launch_bounds__(1024) void sph_sort_local_kernel(
 // sweeps fewer than staging the tile (round 2: load sweep, five chunk sweeps, store sweep).
 // Same compare-swaps in the same pass order as the reference's dispatch sequence.
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ void cas(uint2& lo, uint2& hi) {
-  if (lo.x > hi.x) {
-    const uint2 t = lo;
-    lo = hi;
-    hi = t;
-  }
+// Compare-swap (lower position first): swap when lo.x > hi.x, equal keys stay.  Independent
+// pairs go in batches: every compare first (one mask per pair), then each pair's two
+// v_swap_b32 with its mask as EXEC, EXEC restored at the end -- three VALU ops per pair instead
+// of a compare and four selects, and no branches (2^22 tail 15.9 -> 13.5 us: the in-tile passes
+// are VALU-bound).
+__device__ __forceinline__ void cas(uint2& a, uint2& b) {
+  uint64_t m, sv;
+  asm("v_cmp_gt_u32_e64 %[m], %[ax], %[bx]\n\t"
+      "s_mov_b64 %[sv], exec\n\t"
+      "s_mov_b64 exec, %[m]\n\t"
+      "v_swap_b32 %[ax], %[bx]\n\t"
+      "v_swap_b32 %[ay], %[by]\n\t"
+      "s_mov_b64 exec, %[sv]"
+      : [ax] "+v"(a.x), [bx] "+v"(b.x), [ay] "+v"(a.y), [by] "+v"(b.y), [m] "=&s"(m), [sv] "=&s"(sv));
+}
+__device__ __forceinline__ void cas2(uint2& a0, uint2& b0, uint2& a1, uint2& b1) {
+  uint64_t m0, m1, sv;
+  asm("v_cmp_gt_u32_e64 %[m0], %[a0x], %[b0x]\n\t"
+      "v_cmp_gt_u32_e64 %[m1], %[a1x], %[b1x]\n\t"
+      "s_mov_b64 %[sv], exec\n\t"
+      "s_mov_b64 exec, %[m0]\n\t"
+      "v_swap_b32 %[a0x], %[b0x]\n\t"
+      "v_swap_b32 %[a0y], %[b0y]\n\t"
+      "s_mov_b64 exec, %[m1]\n\t"
+      "v_swap_b32 %[a1x], %[b1x]\n\t"
+      "v_swap_b32 %[a1y], %[b1y]\n\t"
+      "s_mov_b64 exec, %[sv]"
+      : [a0x] "+v"(a0.x), [b0x] "+v"(b0.x), [a0y] "+v"(a0.y), [b0y] "+v"(b0.y),
+        [a1x] "+v"(a1.x), [b1x] "+v"(b1.x), [a1y] "+v"(a1.y), [b1y] "+v"(b1.y),
+        [m0] "=&s"(m0), [m1] "=&s"(m1), [sv] "=&s"(sv));
+}
+__device__ __forceinline__ void cas4(uint2& a0, uint2& b0, uint2& a1, uint2& b1, uint2& a2, uint2& b2,
+                                     uint2& a3, uint2& b3) {
+  uint64_t m0, m1, m2, m3, sv;
+  asm("v_cmp_gt_u32_e64 %[m0], %[a0x], %[b0x]\n\t"
+      "v_cmp_gt_u32_e64 %[m1], %[a1x], %[b1x]\n\t"
+      "v_cmp_gt_u32_e64 %[m2], %[a2x], %[b2x]\n\t"
+      "v_cmp_gt_u32_e64 %[m3], %[a3x], %[b3x]\n\t"
+      "s_mov_b64 %[sv], exec\n\t"
+      "s_mov_b64 exec, %[m0]\n\t"
+      "v_swap_b32 %[a0x], %[b0x]\n\t"
+      "v_swap_b32 %[a0y], %[b0y]\n\t"
+      "s_mov_b64 exec, %[m1]\n\t"
+      "v_swap_b32 %[a1x], %[b1x]\n\t"
+      "v_swap_b32 %[a1y], %[b1y]\n\t"
+      "s_mov_b64 exec, %[m2]\n\t"
+      "v_swap_b32 %[a2x], %[b2x]\n\t"
+      "v_swap_b32 %[a2y], %[b2y]\n\t"
+      "s_mov_b64 exec, %[m3]\n\t"
+      "v_swap_b32 %[a3x], %[b3x]\n\t"
+      "v_swap_b32 %[a3y], %[b3y]\n\t"
+      "s_mov_b64 exec, %[sv]"
+      : [a0x] "+v"(a0.x), [b0x] "+v"(b0.x), [a0y] "+v"(a0.y), [b0y] "+v"(b0.y),
+        [a1x] "+v"(a1.x), [b1x] "+v"(b1.x), [a1y] "+v"(a1.y), [b1y] "+v"(b1.y),
+        [a2x] "+v"(a2.x), [b2x] "+v"(b2.x), [a2y] "+v"(a2.y), [b2y] "+v"(b2.y),
+        [a3x] "+v"(a3.x), [b3x] "+v"(b3.x), [a3y] "+v"(a3.y), [b3y] "+v"(b3.y),
+        [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2), [m3] "=&s"(m3), [sv] "=&s"(sv));
+}
+
+// Entry index of the p-th pair's lower entry in a pass of stride 2^m (bit m cleared).
+__device__ __forceinline__ constexpr int pair_lo(int p, int m) {
+  return ((p >> m) << (m + 1)) | (p & ((1 << m) - 1));
 }
 
 // The non-flip passes of strides g*2^(K-1), ..., g over the 2^K entries v[j] = position
@@ -873,10 +929,21 @@ __device__ __forceinline__ void cas(uint2& lo, uint2& hi) {
 template <int K>
 __device__ __forceinline__ void group_passes(uint2 (&v)[1 << K]) {
 #pragma unroll
-  for (int m = K - 1; m >= 0; --m)
+  for (int m = K - 1; m >= 0; --m) {
+    if constexpr (K == 1) {
+      cas(v[0], v[1]);
+    } else if constexpr (K == 2) {
+      const int d = 1 << m, j0 = pair_lo(0, m), j1 = pair_lo(1, m);
+      cas2(v[j0], v[j0 + d], v[j1], v[j1 + d]);
+    } else {
 #pragma unroll
-    for (int j = 0; j < (1 << K); ++j)
-      if (!(j & (1 << m))) cas(v[j], v[j + (1 << m)]);
+      for (int p = 0; p < (1 << (K - 1)); p += 4) {
+        const int d = 1 << m;
+        const int j0 = pair_lo(p, m), j1 = pair_lo(p + 1, m), j2 = pair_lo(p + 2, m), j3 = pair_lo(p + 3, m);
+        cas4(v[j0], v[j0 + d], v[j1], v[j1 + d], v[j2], v[j2 + d], v[j3], v[j3 + d]);
+      }
+    }
+  }
 }
 
 // Padded LDS index offset of the group's entry j (see above).
@@ -886,8 +953,16 @@ __device__ __forceinline__ constexpr uint32_t pad_off(uint32_t j) {
 }
 __device__ __forceinline__ uint32_t padded(uint32_t e) { return e + (e >> 5); }
 
+// Group i of a thread's 2^LNG in a register chunk: a wave owns the same block of 64 * 2^LNG
+// groups as with q = t * 2^LNG + i (so a chunk inside the wave's entries stays wave-local), but
+// consecutive lanes take consecutive groups: consecutive LDS entries, no bank conflicts.
+template <int LNG>
+__device__ __forceinline__ uint32_t chunk_group(uint32_t t, int i) {
+  return ((t >> 6) << (6 + LNG)) + ((uint32_t)i << 6) + (t & 63u);
+}
+
 // One LDS chunk: passes of strides 2^LG down to 2^(LG-K+1), non-flip, 2^(LE-K) groups per thread
-// (2^LE entries, eight by default), thread t taking groups t * 2^(LE-K) + i.
+// (2^LE entries, eight by default).
 template <int LG, int K, int LE = 3>
 __device__ __forceinline__ void lds_chunk(uint2* lds, uint32_t t) {
   constexpr int LGG = LG - K + 1;
@@ -895,7 +970,7 @@ __device__ __forceinline__ void lds_chunk(uint2* lds, uint32_t t) {
   constexpr int NG = 1 << (LE - K);
 #pragma unroll
   for (int i = 0; i < NG; ++i) {
-    const uint32_t q = t * NG + i;
+    const uint32_t q = chunk_group<LE - K>(t, i);
     const uint32_t e0 = ((q >> LGG) << (LG + 1)) + (q & (g - 1u));
     const uint32_t a = padded(e0);
     uint2 v[1 << K];
@@ -940,6 +1015,40 @@ constexpr int kDppXor1 = 0xB1;  // quad_perm [1, 0, 3, 2]
 constexpr int kDppXor2 = 0x4E;  // quad_perm [2, 3, 0, 1]
 constexpr int kDppRev4 = 0x1B;  // quad_perm [3, 2, 1, 0]
 
+// Quad transpose on pair-index bit B: pair j = (v[2j], v[2j+1]); the pairs whose bit B differs
+// from the lane's bit B trade places with the DPP partner's (lane ^ 2^B) pair j ^ 2^B.
+template <int B, int CTRL>
+__device__ __forceinline__ void quad_swap_bit(uint2 (&v)[8], uint32_t t) {
+  const bool hi = (t >> B) & 1u;
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    constexpr int sh = B == 1 ? 0 : 1;  // position of the pair-index bit that is not B
+    const int j0 = m << sh, j1 = j0 | (1 << B);  // pairs with bit B = 0 / 1
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {  // value selects only: a select of array elements spills v
+      const uint2 x0 = v[2 * j0 + h], x1 = v[2 * j1 + h];
+      const uint32_t ex = hi ? x0.x : x1.x, ey = hi ? x0.y : x1.y;
+      const uint32_t rx = (uint32_t)__builtin_amdgcn_mov_dpp((int)ex, CTRL, 0xF, 0xF, false);
+      const uint32_t ry = (uint32_t)__builtin_amdgcn_mov_dpp((int)ey, CTRL, 0xF, 0xF, false);
+      v[2 * j0 + h] = make_uint2(hi ? rx : x0.x, hi ? ry : x0.y);
+      v[2 * j1 + h] = make_uint2(hi ? x1.x : rx, hi ? x1.y : ry);
+    }
+  }
+}
+
+// Store a lane's eight consecutive entries [8t, 8t + 8) of `tile` in whole 64-B segments: the
+// lane quad transposes its 16-B pairs, so store i of lane l writes pair l of lane i's eight and
+// each store instruction fills one 64-B segment per quad (lane-strided 16-B stores would send
+// four partial write requests per segment).
+__device__ __forceinline__ void store_eight(uint2* tile, uint32_t t, uint2 (&v)[8]) {
+  quad_swap_bit<1, kDppXor2>(v, t);
+  quad_swap_bit<0, kDppXor1>(v, t);
+  uint4* out = reinterpret_cast<uint4*>(tile + 32u * (t >> 2) + 2u * (t & 3u));
+#pragma unroll
+  for (int i = 0; i < 4; ++i) out[4 * i] = make_uint4(v[2 * i].x, v[2 * i].y, v[2 * i + 1].x, v[2 * i + 1].y);
+}
+
+
 template <int TLOG>
 __global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_eu(4))) void sph_sort_tail_kernel(uint2* __restrict__ lookup) {
   static_assert(TLOG >= 10 && TLOG <= 13, "eight entries per thread, 128..1024 threads");
@@ -965,9 +1074,7 @@ __global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_e
     for (int i = 0; i < 8; ++i) v[i] = lds[a + i];
     xlane_pass<kDppXor1, false>(v, (t & 1u) == 0u);  // stride 8: entry i of the left lane vs the right's
     group_passes<3>(v);  // strides 4, 2, 1 inside the lane's eight
-    uint4* out = reinterpret_cast<uint4*>(tile + 8u * t);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) out[i] = make_uint4(v[2 * i].x, v[2 * i].y, v[2 * i + 1].x, v[2 * i + 1].y);
+    store_eight(tile, t, v);
   }
 }
 
@@ -986,24 +1093,12 @@ __global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_e
 
 // Stages 0-2 (spans 2, 4, 8): inside the lane's eight consecutive entries.
 __device__ __forceinline__ void reg_stages012(uint2 (&v)[8]) {
-#pragma unroll
-  for (int i = 0; i < 8; i += 2) cas(v[i], v[i + 1]);  // stage 0: flip G = 1
-#pragma unroll
-  for (int b = 0; b < 8; b += 4) {  // stage 1: flip G = 2, then G = 1
-    cas(v[b], v[b + 3]);
-    cas(v[b + 1], v[b + 2]);
-  }
-#pragma unroll
-  for (int i = 0; i < 8; i += 2) cas(v[i], v[i + 1]);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) cas(v[j], v[7 - j]);  // stage 2: flip G = 4, then G = 2, 1
-#pragma unroll
-  for (int b = 0; b < 8; b += 4) {
-    cas(v[b], v[b + 2]);
-    cas(v[b + 1], v[b + 3]);
-  }
-#pragma unroll
-  for (int i = 0; i < 8; i += 2) cas(v[i], v[i + 1]);
+  cas4(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);  // stage 0: flip G = 1
+  cas4(v[0], v[3], v[1], v[2], v[4], v[7], v[5], v[6]);  // stage 1: flip G = 2, then G = 1
+  cas4(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
+  cas4(v[0], v[7], v[1], v[6], v[2], v[5], v[3], v[4]);  // stage 2: flip G = 4, then G = 2, 1
+  cas4(v[0], v[2], v[1], v[3], v[4], v[6], v[5], v[7]);
+  cas4(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
 }
 
 // The flip chunk of stage S >= 5 in LDS: the flip pass (G = 2^S) and stride 2^(S-1), on the
@@ -1020,16 +1115,9 @@ __device__ __forceinline__ void lds_flip_chunk(uint2* lds, uint32_t t) {
     v[j] = lds[a + pad_off<g>(j)];
     v[4 + j] = lds[b + pad_off<g>(j)];
   }
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {  // flip: position r + j*g pairs with (g-1-r) + (3-j)*g
-    cas(v[j], v[7 - j]);
-    cas(v[4 + j], v[3 - j]);
-  }
-#pragma unroll
-  for (int c = 0; c < 8; c += 4) {  // stride g inside each class
-    cas(v[c], v[c + 1]);
-    cas(v[c + 2], v[c + 3]);
-  }
+  // flip: position r + j*g pairs with (g-1-r) + (3-j)*g; then stride g inside each class
+  cas4(v[0], v[7], v[1], v[6], v[4], v[3], v[5], v[2]);
+  cas4(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     lds[a + pad_off<g>(j)] = v[j];
@@ -1082,43 +1170,25 @@ __device__ __forceinline__ void head_stages(uint2* lds, uint32_t t, uint2 (&v)[8
   }
 }
 
-// The bin pass's inputs for a tile (entry pairs q = 2t + 2k*NT): positions, or the previous
-// frame's pad entries [n, P) (the reference never rewrites them).
-struct BinLoads {
-  f2 pa[4], pc[4];
-  uint4 lk[4];
-};
+// The bin pass's inputs for a tile (entries q = t + k*NT: a wave's loads and its offsets / run2
+// resets cover consecutive particles): positions, or the previous frame's pad entries [n, P)
+// (the reference never rewrites them).
 template <uint32_t NT>
 __device__ __forceinline__ void bin_load(const uint2* lookup, const SortBin& bin, uint32_t base0, uint32_t t,
-                                         BinLoads& in) {
+                                         uint2 (&raw)[8]) {
 #pragma unroll
-  for (uint32_t k = 0; k < 4; ++k) {
-    const uint32_t gq = base0 + 2u * t + k * 2u * NT;
-    if (gq < bin.n) {
-      in.pa[k] = bin_pos(bin, gq);
-      if (gq + 1u < bin.n) in.pc[k] = bin_pos(bin, gq + 1u);
-      else in.lk[k] = *reinterpret_cast<const uint4*>(lookup + gq);
-    } else {
-      in.lk[k] = *reinterpret_cast<const uint4*>(lookup + gq);
-    }
+  for (uint32_t k = 0; k < 8; ++k) {
+    const uint32_t gq = base0 + t + k * NT;
+    raw[k] = gq < bin.n ? __builtin_bit_cast(uint2, bin_pos(bin, gq)) : lookup[gq];
   }
 }
 template <uint32_t NT>
-__device__ __forceinline__ void bin_keys(const SortBin& bin, uint32_t base0, uint32_t t, const BinLoads& in,
+__device__ __forceinline__ void bin_keys(const SortBin& bin, uint32_t base0, uint32_t t, const uint2 (&raw)[8],
                                          const PaddedTile& s) {
 #pragma unroll
-  for (uint32_t k = 0; k < 4; ++k) {
-    const uint32_t q = 2u * t + k * 2u * NT, gq = base0 + q;
-    uint2 a, c;
-    if (gq < bin.n) {
-      a = bin_key(bin, in.pa[k], gq);
-      c = gq + 1u < bin.n ? bin_key(bin, in.pc[k], gq + 1u) : make_uint2(in.lk[k].z, in.lk[k].w);
-    } else {
-      a = make_uint2(in.lk[k].x, in.lk[k].y);
-      c = make_uint2(in.lk[k].z, in.lk[k].w);
-    }
-    s[q] = a;
-    s[q + 1u] = c;
+  for (uint32_t k = 0; k < 8; ++k) {
+    const uint32_t q = t + k * NT, gq = base0 + q;
+    s[q] = gq < bin.n ? bin_key(bin, __builtin_bit_cast(f2, raw[k]), gq) : raw[k];
   }
 }
 
@@ -1131,9 +1201,9 @@ __global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_e
   const uint32_t t = threadIdx.x;
   const uint32_t base0 = blockIdx.x * TILE;
   {  // bin: every position (or pad entry) load first, then the keys
-    BinLoads in;
-    bin_load<NT>(lookup, bin, base0, t, in);
-    bin_keys<NT>(bin, base0, t, in, s);
+    uint2 raw[8];
+    bin_load<NT>(lookup, bin, base0, t, raw);
+    bin_keys<NT>(bin, base0, t, raw, s);
   }
   __syncthreads();
   uint2 v[8];
@@ -1148,9 +1218,7 @@ __global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_e
   // The bin's LDS image was read back by this lane only ([8t, 8t + 8)); its other entries were
   // written by other waves before the barrier above, so stage 5's first write is safe.
   head_stages<5, TLOG>(lds, t, v);
-  uint4* out = reinterpret_cast<uint4*>(lookup + base0 + 8u * t);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) out[i] = make_uint4(v[2 * i].x, v[2 * i].y, v[2 * i + 1].x, v[2 * i + 1].y);
+  store_eight(lookup + base0, t, v);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1170,7 +1238,7 @@ __device__ __forceinline__ void lds_chunk_out(const uint2* lds, uint32_t t, Stor
   constexpr int NG = 1 << (LE - K);
 #pragma unroll
   for (int i = 0; i < NG; ++i) {
-    const uint32_t q = t * NG + i;
+    const uint32_t q = chunk_group<LE - K>(t, i);
     const uint32_t e0 = ((q >> LGG) << (LG + 1)) + (q & (g - 1u));
     const uint32_t a = padded(e0);
     uint2 v[1 << K];
@@ -1224,17 +1292,18 @@ __global__ __launch_bounds__(1u << (T + LW + 1 - LE)) __attribute__((amdgpu_wave
       v[M + j] = lookup[pos(gp - 1u - t + j * gp)];
     }
 #pragma unroll
-    for (int j = 0; j < M / 2; ++j) {  // flip: position t + j*gp pairs with (gp-1-t) + (M-1-j)*gp
-      cas(v[j], v[2 * M - 1 - j]);
-      cas(v[M + j], v[M - 1 - j]);
-    }
+    for (int j = 0; j < M / 2; j += 2)  // flip: position t + j*gp pairs with (gp-1-t) + (M-1-j)*gp
+      cas4(v[j], v[2 * M - 1 - j], v[M + j], v[M - 1 - j], v[j + 1], v[2 * M - 2 - j], v[M + j + 1],
+           v[M - 2 - j]);
 #pragma unroll
     for (int m = KF - 2; m >= 0; --m)  // strides gp * 2^m inside each class
 #pragma unroll
       for (int c = 0; c < 2 * M; c += M)
 #pragma unroll
-        for (int j = 0; j < M; ++j)
-          if (!(j & (1 << m))) cas(v[c + j], v[c + j + (1 << m)]);
+        for (int p = 0; p < M / 2; p += 2) {
+          const int d = 1 << m, j0 = c + pair_lo(p, m), j1 = c + pair_lo(p + 1, m);
+          cas2(v[j0], v[j0 + d], v[j1], v[j1 + d]);
+        }
     const uint32_t a = padded(t), b = padded(gp - 1u - t);
 #pragma unroll
     for (int j = 0; j < M; ++j) {

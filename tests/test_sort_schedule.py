@@ -88,7 +88,9 @@ def mid_chunks(lds, nt, LG):
         LG -= K
 
 
-def tail(tile, TLOG):
+def tail16(tile, TLOG):
+    """The sixteen-entries-per-thread tail (measured slower than the eight-entry kernel: DESIGN.md
+    Appendix A); kept as a replayed alternative."""
     nt = 1 << (TLOG - 4)
     t = np.arange(nt)
     ia = t[:, None] + np.arange(16)[None, :] * nt
@@ -99,6 +101,25 @@ def tail(tile, TLOG):
     mid_chunks(lds, nt, TLOG - 5)
     v = lds[16 * t[:, None] + np.arange(16)[None, :]].copy()
     reg_tail(v, t, 8)
+    return v.reshape(-1, 2)
+
+
+def tail(tile, TLOG):
+    """sph_sort_tail_kernel<TLOG> (rps_kernels.hip): eight entries per thread."""
+    nt = 1 << (TLOG - 3)
+    t = np.arange(nt)
+    v = tile[t[:, None] + np.arange(8)[None, :] * nt].copy()
+    group_passes(v, 3)
+    lds = np.zeros_like(tile)
+    lds[t[:, None] + np.arange(8)[None, :] * nt] = v
+    LG = TLOG - 4
+    while LG >= 4:
+        K = 3 if LG - 3 >= 3 else LG - 3
+        lds_chunk(lds, nt, LG, K)
+        LG -= K
+    v = lds[8 * t[:, None] + np.arange(8)[None, :]].copy()
+    xlane(v, t ^ 1, False, (t & 1) == 0)
+    group_passes(v, 3)
     return v.reshape(-1, 2)
 
 
@@ -114,6 +135,49 @@ def lane_stage(v, S):
 
 
 def head(tile, TLOG):
+    """sph_sort_head_kernel<TLOG> after the bin (rps_kernels.hip): eight entries per thread."""
+    nt = 1 << (TLOG - 3)
+    t = np.arange(nt)
+    v = tile.reshape(nt, 8, 2).copy()
+    for pairs in ([(0, 1), (2, 3), (4, 5), (6, 7)], [(0, 3), (1, 2), (4, 7), (5, 6)],  # reg_stages012
+                  [(0, 1), (2, 3), (4, 5), (6, 7)], [(0, 7), (1, 6), (2, 5), (3, 4)],
+                  [(0, 2), (1, 3), (4, 6), (5, 7)], [(0, 1), (2, 3), (4, 5), (6, 7)]):
+        for i, j in pairs:
+            cas(v, i, j)
+    xlane(v, t ^ 1, True, (t & 1) == 0)  # stage 3
+    group_passes(v, 3)
+    xlane(v, t ^ 3, True, (t & 2) == 0)  # stage 4
+    xlane(v, t ^ 1, False, (t & 1) == 0)
+    group_passes(v, 3)
+    lds = np.zeros_like(tile)
+    own = 8 * t[:, None] + np.arange(8)[None, :]
+    for S in range(5, TLOG):
+        lds[own] = v
+        g = 1 << (S - 1)
+        LP = S - 2
+        base = (t >> LP) << (S + 1)
+        r = t & ((1 << LP) - 1)
+        ia = base[:, None] + r[:, None] + np.arange(4)[None, :] * g
+        ib = base[:, None] + (g - 1 - r)[:, None] + np.arange(4)[None, :] * g
+        w = np.concatenate([lds[ia], lds[ib]], 1)
+        for i, j in ((0, 7), (1, 6), (4, 3), (5, 2), (0, 1), (2, 3), (4, 5), (6, 7)):  # lds_flip_chunk
+            cas(w, i, j)
+        lds[ia], lds[ib] = w[:, :4], w[:, 4:]
+        LG = S - 2
+        while LG >= 5:
+            K = 3 if LG - 4 >= 3 else LG - 4
+            lds_chunk(lds, nt, LG, K)
+            LG -= K
+        v = lds[own].copy()
+        if S >= 6:
+            xlane(v, t ^ 2, False, (t & 2) == 0)
+        xlane(v, t ^ 1, False, (t & 1) == 0)
+        group_passes(v, 3)
+    return v.reshape(-1, 2)
+
+
+def head16(tile, TLOG):
+    """The sixteen-entries-per-thread head (measured slower); kept as a replayed alternative."""
     nt = 1 << (TLOG - 4)
     t = np.arange(nt)
     v = tile.reshape(nt, 16, 2).copy()
@@ -166,18 +230,52 @@ def store_sixteen(v, t):
     return out
 
 
-@pytest.mark.parametrize("TLOG", [10, 11, 12, 13])
+def quad_swap_bit(pairs, B):
+    """quad_swap_bit<B> over every lane: lane l trades the pairs whose index bit B differs from
+    its own bit B with lane l ^ 2^B's pair j ^ 2^B (pairs: [lane, pair, 2, 2])."""
+    out = pairs.copy()
+    for ln in range(len(pairs)):
+        p = ln ^ (1 << B)
+        for j in range(4):
+            if ((j >> B) & 1) != ((ln >> B) & 1):
+                out[ln, j] = pairs[p, j ^ (1 << B)]
+    return out
+
+
+def store_eight(v):
+    """store_eight: the two quad_swap_bit steps, then store m of lane l = 4q + l' at entry
+    32q + 8m + 2l' (one whole 64-B segment per quad and store instruction)."""
+    nt = len(v)
+    pairs = quad_swap_bit(quad_swap_bit(v.reshape(nt, 4, 2, 2), 1), 0)
+    out = np.full((nt * 8, 2), -1, dtype=v.dtype)
+    for ln in range(nt):
+        for m in range(4):
+            dst = 32 * (ln >> 2) + 8 * m + 2 * (ln & 3)
+            out[dst:dst + 2] = pairs[ln, m]
+    return out
+
+
+def test_store_eight_writes_each_lane_to_its_entries():
+    """Lane t's eight entries [8t, 8t + 8) land there after the DPP transposition."""
+    v = np.stack([np.arange(512), 1000 + np.arange(512)], 1).reshape(64, 8, 2)
+    np.testing.assert_array_equal(store_eight(v), v.reshape(-1, 2))
+
+
+@pytest.mark.parametrize("TLOG", [11, 12, 13])
 @pytest.mark.parametrize("kmax", [7, 1 << 20])
-def test_head_schedule_equals_network(TLOG, kmax):
+@pytest.mark.parametrize("layout", ["eight", "sixteen"])
+def test_head_schedule_equals_network(TLOG, kmax, layout):
     g = np.random.default_rng(TLOG * 7 + (kmax & 3))
     keys = g.integers(0, kmax, 1 << TLOG)  # kmax 7: dense ties; 2^20: mostly distinct
     tile = np.stack([keys, np.arange(len(keys))], 1).astype(np.int64)
-    np.testing.assert_array_equal(head(tile, TLOG), ref_network(keys, TLOG))
+    run = head if layout == "eight" else head16
+    np.testing.assert_array_equal(run(tile, TLOG), ref_network(keys, TLOG))
 
 
-@pytest.mark.parametrize("TLOG", [10, 11, 12, 13])
+@pytest.mark.parametrize("TLOG", [11, 12, 13])
 @pytest.mark.parametrize("kmax", [7, 1 << 20])
-def test_tail_schedule_equals_network(TLOG, kmax):
+@pytest.mark.parametrize("layout", ["eight", "sixteen"])
+def test_tail_schedule_equals_network(TLOG, kmax, layout):
     """A later stage s's passes inside one tile: strides 2^(TLOG-1) .. 1, non-flip (the tile
     after the stage's global passes; any input order)."""
     g = np.random.default_rng(TLOG * 11 + (kmax & 5))
@@ -196,7 +294,7 @@ def test_tail_schedule_equals_network(TLOG, kmax):
         sw = a[left, 0] > a[right, 0]
         l, r = a[left[sw]].copy(), a[right[sw]].copy()
         a[left[sw]], a[right[sw]] = r, l
-    np.testing.assert_array_equal(tail(tile, TLOG), a)
+    np.testing.assert_array_equal((tail if layout == "eight" else tail16)(tile, TLOG), a)
 
 
 def test_store_sixteen_places_each_lane_contiguously():
