@@ -57,6 +57,16 @@ struct rps_ctx {
   bool layout_last = false;  // the last active frame used the layout (slot records in storage order)
   bool last_frame_active = false;  // the most recent frame ran passes 4-5 (rps_sph_frame_cost)
   unsigned long long* d_count = nullptr;  // rps_sph_frame_cost's per-workgroup counts (SPH)
+  // Slot-resident state (layout frames): after a layout frame st holds the
+  // state in that frame's storage order, perm = sl.idx_s (slot -> particle), and bin_next the
+  // next frame's bin entries.  Every API call that reads or writes particles in particle order
+  // first puts the state back (sph_canonical).
+  f4* st_alt = nullptr;         // particle-order target of sph_canonical (swapped with st)
+  uint32_t* idx_alt = nullptr;  // the other slot -> particle buffer (alternates with sl.idx_s)
+  uint2* bin_next = nullptr;
+  bool resident = false;
+  bool keys_valid = false;      // bin_next matches st and the current config
+  const uint32_t* lookup_perm = nullptr;  // the lookup's payloads are slots of this perm
   // N-body
   f2* pos_all = nullptr;
   uint64_t ns_padded = 0;
@@ -280,6 +290,9 @@ SphBuffers sph_buffers(rps_ctx* ctx) {
   SphBuffers b;
   b.cfg = ctx->d_cfg;
   b.st = ctx->st;
+  b.bin_next = ctx->bin_next;
+  b.idx_prev = ctx->idx_alt;  // during a resident frame: the perm its sort payloads refer to
+  b.resident = ctx->resident;
   b.sl = ctx->sl;
   b.ends = ctx->ends;
   b.lookup = ctx->lookup;
@@ -444,6 +457,35 @@ int step_sph_grid(rps_ctx* ctx, bool active) {
   return RPS_OK;
 }
 
+// The state back in particle order (st_alt[perm[u]] = st[u], then the buffers swap).
+int sph_canonical(rps_ctx* ctx) {
+  if (!ctx->resident) return RPS_OK;
+  RPS_HIP(ctx, launch_sph_materialize(ctx->st, ctx->sl.idx_s, ctx->st_alt, (uint32_t)ctx->n, ctx->stream));
+  std::swap(ctx->st, ctx->st_alt);
+  set_sph_fields(ctx);
+  ctx->resident = false;
+  ctx->keys_valid = false;
+  return RPS_OK;
+}
+
+// Before a frame's passes 1-3: a frame that does not use the layout needs particle order; a
+// resident frame whose bin entries are stale (config changed) rebuilds them from the state;
+// a resident frame writes its slot -> particle map to the other buffer (the sort payloads
+// refer to the current one).
+int sph_frame_begin(rps_ctx* ctx, bool layout) {
+  if (ctx->resident && !layout) {
+    const int rc = sph_canonical(ctx);
+    if (rc) return rc;
+  }
+  if (ctx->resident && !ctx->keys_valid) {
+    RPS_HIP(ctx, launch_sph_rebin(sph_buffers(ctx), ctx->sl.idx_s, ctx->stream));
+    ctx->keys_valid = true;
+  }
+  ctx->lookup_perm = ctx->resident ? ctx->sl.idx_s : nullptr;
+  if (ctx->resident) std::swap(ctx->sl.idx_s, ctx->idx_alt);
+  return RPS_OK;
+}
+
 int step_sph_sim(rps_ctx* ctx, bool layout, const SphGrid& g) {
   ctx->layout_last = layout;
   if (layout) ctx->lay.g = g;
@@ -457,6 +499,10 @@ int step_sph_sim(rps_ctx* ctx, bool layout, const SphGrid& g) {
   RPS_HIP(ctx, launch_sph_sim(b, ctx->stream));
   rc = prof_end(ctx);
   if (rc) return rc;
+  if (layout) {  // the sim wrote st in this frame's slot order and the next bin entries
+    ctx->resident = true;
+    ctx->keys_valid = true;
+  }
   return RPS_OK;
 }
 
@@ -594,6 +640,9 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
       slots.push_back({(void**)&ctx->lay.part, align_up((cap / 256 + 2) * sizeof(uint32_t), 256)});
       slots.push_back({(void**)&ctx->lay.out_runs, align_up(n * sizeof(uint2), 256)});
       slots.push_back({(void**)&ctx->lay.n_out, 256});
+      slots.push_back({(void**)&ctx->st_alt, align_up(n * sizeof(f4), 256)});
+      slots.push_back({(void**)&ctx->idx_alt, align_up(P * sizeof(uint32_t), 256)});
+      slots.push_back({(void**)&ctx->bin_next, align_up(n * sizeof(uint2), 256)});
     }
   }
   if (ctx->mode == RPS_MODE_NBODY) {
@@ -694,6 +743,7 @@ int rps_set_config(rps_ctx* ctx, const rps_config* cfg, const rps_ext_config* ex
   ctx->cfg = *cfg;
   ctx->ext = e;
   ctx->have_config = true;
+  ctx->keys_valid = false;  // slot-resident bin entries were keyed with the old config
   // write_buffer(config) (src/particle_buffers.rs:230-236): the 144 B ride in a one-wave
   // kernel's arguments, ordered on the context stream before the next step's kernels.  A
   // pinned-staging hipMemcpyAsync cost 12-18 us a frame at 65 536 particles (STREAM) and
@@ -716,6 +766,7 @@ int rps_upload_particles(rps_ctx* ctx, const rps_particle* aos, uint64_t offset,
   if (offset + n > ctx->n) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "range exceeds particle_count");
   const uint64_t chunk = std::min<uint64_t>(n, kStagingChunk);
   if (n == 0) return RPS_OK;
+  if ((rc = sph_canonical(ctx))) return rc;
   rc = ensure_staging(ctx, chunk);
   if (rc) return rc;
   for (uint64_t done = 0; done < n; done += chunk) {
@@ -735,6 +786,7 @@ int rps_download_particles(rps_ctx* ctx, rps_particle* aos, uint64_t offset, uin
   if (!aos && n) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "null particles");
   if (offset + n > ctx->n) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "range exceeds particle_count");
   if (n == 0) return RPS_OK;
+  if ((rc = sph_canonical(ctx))) return rc;
   const uint64_t chunk = std::min<uint64_t>(n, kStagingChunk);
   rc = ensure_staging(ctx, chunk);
   if (rc) return rc;
@@ -761,6 +813,7 @@ int rps_export_particles(rps_ctx* ctx, rps_particle* device_dst, uint64_t offset
     if (pe != hipSuccess) (void)hipGetLastError();  // do not leave a sticky error for later launches
     if (pe != hipSuccess || attr.type != hipMemoryTypeDevice)
       return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "device_dst is not device memory");
+    if ((rc = sph_canonical(ctx))) return rc;
   }
   constexpr uint64_t kChunk = 1ull << 30;  // stays under the 2^31 work-item grid cap
   for (uint64_t done = 0; done < n; done += kChunk) {
@@ -782,6 +835,8 @@ int rps_upload_field(rps_ctx* ctx, int field, const float* src, uint64_t offset,
   if (!src && n) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "null source");
   if (offset + n > ctx->n) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "range exceeds particle_count");
   if (n == 0) return RPS_OK;
+  if ((rc = sph_canonical(ctx))) return rc;
+  if (!life) p = field_ptr(ctx, field);  // (sph_canonical may have swapped the state buffer)
   if (!life && ctx->layout.mask == plain_layout().mask) {
     RPS_HIP(ctx, hipMemcpyAsync(p + offset, src, n * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
     RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -819,6 +874,8 @@ int rps_download_field(rps_ctx* ctx, int field, float* dst, uint64_t offset, uin
   if (!dst && n) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "null destination");
   if (offset + n > ctx->n) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "range exceeds particle_count");
   if (n == 0) return RPS_OK;
+  if ((rc = sph_canonical(ctx))) return rc;
+  if (!life) p = field_ptr(ctx, field);  // (sph_canonical may have swapped the state buffer)
   if (!life && ctx->layout.mask == plain_layout().mask) {
     RPS_HIP(ctx, hipMemcpyAsync(dst, p + offset, n * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
     RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -878,6 +935,13 @@ int rps_read_debug(rps_ctx* ctx, int which, void* dst, uint64_t bytes) {
   }
   if (which == RPS_DEBUG_DENSITIES || which == RPS_DEBUG_PREDICTED)
     RPS_HIP(ctx, launch_sph_debug_views(sph_buffers(ctx), ctx->stream));
+  if (which == RPS_DEBUG_SPATIAL_LOOKUP && ctx->lookup_perm) {
+    // Slot-resident frame: payloads are the previous frame's slots; the reference holds
+    // particle indices.  Translated into out_runs (free between frames, P == N entries).
+    RPS_HIP(ctx, launch_sph_lookup_translate(ctx->lookup, ctx->lookup_perm, ctx->lay.out_runs, ctx->P,
+                                             ctx->stream));
+    src = ctx->lay.out_runs;
+  }
   // A spatial-layout frame measures its runs without writing the reference's offsets (the bin
   // pass reset them): pass 3 (wgsl:507-525) on the frame's sorted lookup, on demand.
   if (which == RPS_DEBUG_LOOKUP_OFFSETS && ctx->layout_last)
@@ -908,6 +972,8 @@ int rps_init_scatter(rps_ctx* ctx, uint64_t seed) {
   a.dt = ctx->cfg.fixed_delta_time;
   a.key0 = (uint32_t)seed;
   a.key1 = (uint32_t)(seed >> 32);
+  ctx->resident = false;  // every particle rewritten in particle order
+  ctx->keys_valid = false;
   RPS_HIP(ctx, launch_init_scatter(a, ctx->stream));
   if (ctx->next)
     RPS_HIP(ctx, launch_next_rebuild(ctx->exp, ctx->next, 0, ctx->n, ctx->n, (uint32_t)ctx->life_clock,
@@ -936,6 +1002,8 @@ int rps_step(rps_ctx* ctx, uint32_t nsteps) {
     SphGrid grid{};
     const bool layout = ctx->mode == RPS_MODE_SPH && active && sph_layout_grid(ctx->cfg, ctx->cell_cap, &grid);
     if (ctx->mode == RPS_MODE_SPH) {
+      rc = sph_frame_begin(ctx, layout);
+      if (rc) return rc;
       // passes 1-3 run every frame (particle_compute.rs:105-163); on an active frame the
       // offsets pass rides in the next kernel (the layout's runs kernel or predict)
       rc = step_sph_grid(ctx, active);

@@ -135,6 +135,14 @@ struct SphBuffers {
   f2* dens;          // N  debug views (wgsl:58, :61), rebuilt on readback
   f2* pred;          // N
   SphSlots sl;
+  // Slot-resident state: after a layout frame `st` holds the state in that
+  // frame's storage order (slot u: particle perm[u]) and bin_next the next frame's bin entries
+  // (key, u) at position i.  With `resident`, this frame's sort payloads are those slots and
+  // idx_prev (= perm) maps them to particle indices; the sim of a layout frame writes st[u]
+  // and bin_next.
+  uint2* bin_next;   // N
+  const uint32_t* idx_prev;  // N (resident only)
+  bool resident;
   uint32_t n;        // N
   uint32_t p;        // next_pow2(N)
   uint8_t batch_d;   // scan entries in flight per lane, density / sim pass (4, 8, 16;
@@ -166,5 +174,11 @@ uint32_t sph_count_blocks(uint32_t p_slots);
 hipError_t launch_sph_count(const SphBuffers& b, unsigned long long* out, hipStream_t s);
 // Rebuild the per-particle predicted-position and density buffers from the slot records.
 hipError_t launch_sph_debug_views(const SphBuffers& b, hipStream_t s);
+// Slot-resident state: bin_next from the state (keys of the current config), the state back to
+// particle order (dst[perm[u]] = st[u]), and the sorted lookup's payloads as particle indices.
+hipError_t launch_sph_rebin(const SphBuffers& b, const uint32_t* perm, hipStream_t s);
+hipError_t launch_sph_materialize(const f4* st, const uint32_t* perm, f4* dst, uint32_t n, hipStream_t s);
+hipError_t launch_sph_lookup_translate(const uint2* lookup, const uint32_t* perm, uint2* out, uint32_t p,
+                                       hipStream_t s);
 
 }  // namespace rps

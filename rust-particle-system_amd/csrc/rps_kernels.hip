@@ -660,17 +660,19 @@ struct SortBin {
   uint32_t* offsets;
   uint32_t n;
   uint2* run2;  // spatial layout's storage runs, reset with offsets (nullptr: no layout)
+  const uint2* prebuilt;  // bin entries the previous frame's sim wrote (nullptr: from positions)
 };
 
 __device__ __forceinline__ f2 bin_pos(const SortBin& b, uint32_t i) {
   return reinterpret_cast<const f2*>(b.st)[2u * i];
 }
 __device__ __forceinline__ uint2 bin_key(const SortBin& b, f2 pos, uint32_t i) {
+  b.offsets[i] = 0xFFFFFFFFu;
+  if (b.run2) b.run2[i] = make_uint2(0xFFFFFFFFu, 0u);
+  if (b.prebuilt) return b.prebuilt[i];  // slot-resident state: (key, slot), keyed by the sim
   const float r = b.cfg->smoothing_radius;
   const int32_t cx = f32_to_i32((pos[0] + b.cfg->screen_bounds[1]) / r);
   const int32_t cy = f32_to_i32((pos[1] + b.cfg->screen_bounds[3]) / r);
-  b.offsets[i] = 0xFFFFFFFFu;
-  if (b.run2) b.run2[i] = make_uint2(0xFFFFFFFFu, 0u);
   return make_uint2(cell_key(cx, cy, b.cfg->particle_count), i);
 }
 __device__ __forceinline__ uint2 bin_entry(const SortBin& b, uint32_t i) {
@@ -1179,7 +1181,7 @@ __device__ __forceinline__ void bin_load(const uint2* lookup, const SortBin& bin
 #pragma unroll
   for (uint32_t k = 0; k < 8; ++k) {
     const uint32_t gq = base0 + t + k * NT;
-    raw[k] = gq < bin.n ? __builtin_bit_cast(uint2, bin_pos(bin, gq)) : lookup[gq];
+    raw[k] = gq >= bin.n ? lookup[gq] : bin.prebuilt ? bin.prebuilt[gq] : __builtin_bit_cast(uint2, bin_pos(bin, gq));
   }
 }
 template <uint32_t NT>
@@ -1188,7 +1190,15 @@ __device__ __forceinline__ void bin_keys(const SortBin& bin, uint32_t base0, uin
 #pragma unroll
   for (uint32_t k = 0; k < 8; ++k) {
     const uint32_t q = t + k * NT, gq = base0 + q;
-    s[q] = gq < bin.n ? bin_key(bin, __builtin_bit_cast(f2, raw[k]), gq) : raw[k];
+    if (gq >= bin.n) {
+      s[q] = raw[k];
+    } else if (bin.prebuilt) {  // (key, slot): the resets of bin_key only
+      bin.offsets[gq] = 0xFFFFFFFFu;
+      if (bin.run2) bin.run2[gq] = make_uint2(0xFFFFFFFFu, 0u);
+      s[q] = raw[k];
+    } else {
+      s[q] = bin_key(bin, __builtin_bit_cast(f2, raw[k]), gq);
+    }
   }
 }
 
@@ -1400,9 +1410,13 @@ __constant__ int32_t kGridOff[9][2] = {{-1, -1}, {-1, 0}, {-1, 1}, {0, -1}, {0, 
 // from the slot records on readback.  Pad slots repeat some particle and
 // write identical values.
 // apply_gravity (wgsl:397-400) and the prediction (:402-405) of particle i into slot u.
+// `e` is the sort payload: the particle index, or with slot-resident state the particle's slot
+// in st (its index then idx_prev[e]).
 __device__ __forceinline__ void predict_slot(const rps_config* __restrict__ cfg, const f4* __restrict__ st,
-                                             const SphSlots& sl, uint32_t u, uint32_t i) {
-  const f4 s = st[i];
+                                             const SphSlots& sl, uint32_t u, uint32_t e,
+                                             const uint32_t* __restrict__ idx_prev = nullptr) {
+  const f4 s = st[e];
+  const uint32_t i = idx_prev ? idx_prev[e] : e;
   const float dt = cfg->fixed_delta_time;
   const float qx = s[2] + 0.0f * dt;  // apply_gravity, wgsl:397-400
   const float qy = s[3] + (-cfg->gravity) * dt;
@@ -1682,7 +1696,7 @@ __device__ __forceinline__ void scan_runs(const SphSlots& sl, const RunTable& ru
 template <int kScanBatch, bool kPads, bool LAYOUT>
 __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __restrict__ cfg,
                                                          RunBounds rb, SphSlots sl, f4* __restrict__ st,
-                                                         uint32_t p_slots) {
+                                                         uint2* __restrict__ bin_next, uint32_t p_slots) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= p_slots) return;
   const f4 own = sl.rec_pd[t];  // own predicted position (xy) and P / rho^2 (z)
@@ -1761,7 +1775,17 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
   float oy = c[1] + qy * dt;
   wall(cfg->screen_bounds[0], cfg->screen_bounds[1], cfg->screen_bounds[2], cfg->screen_bounds[3],
        cfg->damping_factor, ox, oy, qx, qy);
-  st[i] = f4{ox, oy, qx, qy};
+  if (LAYOUT) {
+    // Slot-resident state: the new state at its slot (a coalesced store instead of a 16-B
+    // scatter), and the next frame's bin entry of particle i (bin_key's ops on the same
+    // position and config), which the next head launch reads in place of the positions.
+    st[t] = f4{ox, oy, qx, qy};
+    const int32_t cx = f32_to_i32((ox + cfg->screen_bounds[1]) / r);
+    const int32_t cy = f32_to_i32((oy + cfg->screen_bounds[3]) / r);
+    bin_next[i] = make_uint2(cell_key(cx, cy, N), t);
+  } else {
+    st[i] = f4{ox, oy, qx, qy};
+  }
 }
 
 // predicted_positions / densities (wgsl:58, :61) rebuilt from the slot records for
@@ -1780,6 +1804,36 @@ __global__ __launch_bounds__(kBlock) void sph_debug_views_kernel(SphSlots sl, f2
 // its particle's nine runs (what the reference's density and sim scans visit,
 // wgsl:207-254, :279-384) and how many of them lie within the radius.  One (scanned,
 // within) u64 pair per workgroup, summed on the host; integer sums, so order-free.
+// Slot-resident state (SphBuffers::bin_next): the bin entries from the state itself, with the
+// current config (after rps_set_config), as the sim would have written them.
+__global__ __launch_bounds__(kBlock) void sph_rebin_kernel(const rps_config* __restrict__ cfg,
+                                                           const f4* __restrict__ st,
+                                                           const uint32_t* __restrict__ perm,
+                                                           uint2* __restrict__ bin_next, uint32_t n) {
+  const uint32_t u = blockIdx.x * kBlock + threadIdx.x;
+  if (u >= n) return;
+  const f4 s = st[u];
+  const float r = cfg->smoothing_radius;
+  const int32_t cx = f32_to_i32((s[0] + cfg->screen_bounds[1]) / r);
+  const int32_t cy = f32_to_i32((s[1] + cfg->screen_bounds[3]) / r);
+  bin_next[perm[u]] = make_uint2(cell_key(cx, cy, cfg->particle_count), u);
+}
+// The state back in particle order.
+__global__ __launch_bounds__(kBlock) void sph_materialize_kernel(const f4* __restrict__ st,
+                                                                 const uint32_t* __restrict__ perm,
+                                                                 f4* __restrict__ dst, uint32_t n) {
+  const uint32_t u = blockIdx.x * kBlock + threadIdx.x;
+  if (u < n) dst[perm[u]] = st[u];
+}
+// The sorted lookup with particle indices as payloads (the reference's spatial_lookup).
+__global__ __launch_bounds__(kBlock) void sph_lookup_translate_kernel(const uint2* __restrict__ lookup,
+                                                                      const uint32_t* __restrict__ perm,
+                                                                      uint2* __restrict__ out, uint32_t p) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= p) return;
+  const uint2 e = lookup[t];
+  out[t] = make_uint2(e.x, perm[e.y]);
+}
 __global__ __launch_bounds__(kBlock) void sph_count_kernel(const rps_config* __restrict__ cfg,
                                                            const uint32_t* __restrict__ offsets,
                                                            const uint32_t* __restrict__ ends,
@@ -1976,8 +2030,9 @@ constexpr uint32_t kSlotMap = 2048;
 __global__ __launch_bounds__(kBlock) void sph_layout_write_kernel(SphLayoutArgs a,
                                                                   const rps_config* __restrict__ cfg,
                                                                   const uint2* __restrict__ lookup,
-                                                                  const f4* __restrict__ st, SphSlots sl,
-                                                                  uint32_t N) {
+                                                                  const f4* __restrict__ st,
+                                                                  const uint32_t* __restrict__ idx_prev,
+                                                                  SphSlots sl, uint32_t N) {
   __shared__ uint32_t lbase[kBlock], lsrc[kBlock], lidx[kRunIdx][kBlock];
   __shared__ uint8_t lcell[kSlotMap];
   const uint32_t e = blockIdx.x * kBlock + threadIdx.x;
@@ -2022,7 +2077,7 @@ __global__ __launch_bounds__(kBlock) void sph_layout_write_kernel(SphLayoutArgs 
     }
     const uint32_t r = k - lbase[lo];
     const uint32_t i = r < kRunIdx ? lidx[r][lo] : lookup[lsrc[lo] + r].y;
-    predict_slot(cfg, st, sl, b0 + k, i);
+    predict_slot(cfg, st, sl, b0 + k, i, idx_prev);
   }
   // The listed runs' slots [part[blocks], N), spread over every thread of the launch (one slot
   // per thread at most once the launch covers N: a clump of many particles in one run costs
@@ -2037,7 +2092,7 @@ __global__ __launch_bounds__(kBlock) void sph_layout_write_kernel(SphLayoutArgs 
       else hi = mid;
     }
     const uint2 run = a.out_runs[lo];
-    predict_slot(cfg, st, sl, k, lookup[run.x + (k - run.y)].y);
+    predict_slot(cfg, st, sl, k, lookup[run.x + (k - run.y)].y, idx_prev);
   }
 }
 
@@ -2257,7 +2312,8 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
   while ((1u << stages) < P) ++stages;
   *passes = stages * (stages + 1u) / 2u;
   *launches = 0;
-  const SortBin bin{b.cfg, b.st, b.offsets, b.n, b.lay.run2};
+  // Slot-resident state: the previous layout frame's sim wrote the bin entries (key, slot).
+  const SortBin bin{b.cfg, b.st, b.offsets, b.n, b.lay.run2, b.resident ? b.bin_next : nullptr};
   if (stages == 0) {  // P == 1: nothing to sort, only bin
     hipLaunchKernelGGL((sph_sort_local_kernel<true, 1>), dim3(1), dim3(64), 0, s, b.lookup, 1u, 1u, 0u,
                        0u, bin, 0u);
@@ -2427,7 +2483,7 @@ hipError_t launch_sph_layout_pre(const SphBuffers& b, hipStream_t s) {
   hipLaunchKernelGGL(sph_layout_scan_kernel, dim3(1), dim3(1024), 0, s, a, b.lookup, nparts);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(sph_layout_write_kernel, dim3(nparts), dim3(kBlock), 0, s, a, b.cfg, b.lookup, b.st,
-                     b.sl, b.n);
+                     b.resident ? b.idx_prev : nullptr, b.sl, b.n);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(sph_layout_fixup_kernel, dim3(nparts), dim3(kBlock), 0, s, a, b.n);
   if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -2439,13 +2495,13 @@ hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s) {
 #define RPS_SIM(B)                                                                                  \
   if (b.layout)                                                                                     \
     hipLaunchKernelGGL((sph_sim_kernel<B, false, true>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s, \
-                       b.cfg, rb, b.sl, b.st, b.p);                                           \
+                       b.cfg, rb, b.sl, b.st, b.bin_next, b.p);                                           \
   else if (b.p == b.n)                                                                              \
     hipLaunchKernelGGL((sph_sim_kernel<B, false, false>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s, \
-                       b.cfg, rb, b.sl, b.st, b.p);                                           \
+                       b.cfg, rb, b.sl, b.st, b.bin_next, b.p);                                           \
   else                                                                                              \
     hipLaunchKernelGGL((sph_sim_kernel<B, true, false>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s, \
-                       b.cfg, rb, b.sl, b.st, b.p)
+                       b.cfg, rb, b.sl, b.st, b.bin_next, b.p)
   switch (sph_batch(false, b.p, b.batch_s, b.layout)) {
     case 4: RPS_SIM(4); break;
     case 6: RPS_SIM(6); break;
@@ -2464,6 +2520,19 @@ hipError_t launch_sph_count(const SphBuffers& b, unsigned long long* out, hipStr
   return hipGetLastError();
 }
 
+hipError_t launch_sph_rebin(const SphBuffers& b, const uint32_t* perm, hipStream_t s) {
+  hipLaunchKernelGGL(sph_rebin_kernel, dim3(blocks_for(b.n)), dim3(kBlock), 0, s, b.cfg, b.st, perm, b.bin_next, b.n);
+  return hipGetLastError();
+}
+hipError_t launch_sph_materialize(const f4* st, const uint32_t* perm, f4* dst, uint32_t n, hipStream_t s) {
+  hipLaunchKernelGGL(sph_materialize_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, s, st, perm, dst, n);
+  return hipGetLastError();
+}
+hipError_t launch_sph_lookup_translate(const uint2* lookup, const uint32_t* perm, uint2* out, uint32_t p,
+                                       hipStream_t s) {
+  hipLaunchKernelGGL(sph_lookup_translate_kernel, dim3(blocks_for(p)), dim3(kBlock), 0, s, lookup, perm, out, p);
+  return hipGetLastError();
+}
 hipError_t launch_sph_debug_views(const SphBuffers& b, hipStream_t s) {
   hipLaunchKernelGGL(sph_debug_views_kernel, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.sl,
                      b.pred, b.dens, b.p);

@@ -100,9 +100,12 @@ def test_sph_grid_passes_large(gpu, orc, n):
         assert_bitwise(ctx.read_debug(rps.DEBUG_LOOKUP_OFFSETS), st.offsets, "offsets")
 
 
-def _frames_vs_oracle(rps, orc, n, soa, cfg, frames, cfg_at=None):
+def _frames_vs_oracle(rps, orc, n, soa, cfg, frames, cfg_at=None, download_at=None):
     """Step `frames` SPH frames (shader_delay 0) and check every frame bitwise: lookup,
-    offsets, predicted positions, densities, state.  cfg_at: {frame: new config}."""
+    offsets, predicted positions, densities, state.  cfg_at: {frame: new config};
+    download_at: the frames after which the state is downloaded (default: every frame; the
+    last frame always) -- a download puts slot-resident state back in particle order, so
+    frames between downloads carry it over."""
     ext = rps.make_ext(shader_delay=0)
     st = orc.SphState(n)
     ref = copy_soa(soa)
@@ -121,7 +124,85 @@ def _frames_vs_oracle(rps, orc, n, soa, cfg, frames, cfg_at=None):
             assert_bitwise(ctx.read_debug(rps.DEBUG_PREDICTED), st.pred, f"pred f{frame}")
             assert_bitwise(ctx.read_debug(rps.DEBUG_DENSITIES), st.dens, f"dens f{frame}")
             st.sim(cfg, ref)
-            assert_soa_bitwise(ctx.download_soa(), ref, what=f"f{frame} ")
+            if download_at is None or frame in download_at or frame == frames - 1:
+                assert_soa_bitwise(ctx.download_soa(), ref, what=f"f{frame} ")
+
+
+@pytest.mark.parametrize("n", [16384, 1 << 21])
+def test_sph_resident_state_frames(gpu, orc, monkeypatch, n):
+    """Slot-resident state: after a layout frame the state stays in that
+    frame's storage order and the sim writes the next frame's bin entries.  Consecutive layout
+    frames with no download between them (the debug reads translate the sorted lookup's slot
+    payloads back to particle indices), a config change between resident frames (stale bin
+    entries rebuilt from the state), downloads at frames 3 and 6: every pass bitwise."""
+    rps = gpu
+    monkeypatch.setenv("RPS_SPH_LAYOUT", "2")
+    if n == 16384:
+        cfg = rps.default_particle_config(n, gravity=100.0)
+        soa = _blob(n, 41, spread=300.0)
+        cfg2 = rps.default_particle_config(n, gravity=60.0, smoothing_radius=7.0)
+    else:
+        scale = (n / 50000) ** 0.5
+        bounds = rps.screen_bounds_for(1920.0 * scale, 1080.0 * scale)
+        cfg = rps.default_particle_config(n, screen_bounds=bounds)
+        parts = rps.setup_particles_scatter(cfg, n, seed=0x5EED)
+        soa = dict(x=parts["position"][:, 0].copy(), y=parts["position"][:, 1].copy(),
+                   vx=parts["velocity"][:, 0].copy(), vy=parts["velocity"][:, 1].copy())
+        cfg2 = rps.default_particle_config(n, screen_bounds=bounds, gravity=60.0)
+    _frames_vs_oracle(rps, orc, n, soa, cfg, 7 if n == 16384 else 4, cfg_at={2: cfg2},
+                      download_at={3, 6})
+
+
+def test_sph_resident_state_api(gpu, orc, monkeypatch):
+    """Every particle-order API call on slot-resident state: a device export, a partial field
+    upload, a download, and gated frames (a config change resetting frame_count, SHADER_DELAY
+    3) right after resident frames; the state bitwise after each step, the export bitwise
+    against the oracle's particles."""
+    from hip_mem import DeviceBuffer
+
+    rps = gpu
+    monkeypatch.setenv("RPS_SPH_LAYOUT", "2")
+    n = 16384
+    cfg = rps.default_particle_config(n, gravity=100.0)
+    soa = _blob(n, 43, spread=300.0)
+    st = orc.SphState(n)
+    ref = copy_soa(soa)
+
+    def frames(k, gated=0):
+        for f in range(k):
+            st.grid(cfg, ref)
+            if f >= gated:
+                st.pre(cfg, ref)
+                st.sim(cfg, ref)
+
+    with rps.Context(n, rps.MODE_SPH) as ctx, DeviceBuffer(n * rps.PARTICLE_DTYPE.itemsize) as buf:
+        ctx.set_config(cfg, rps.make_ext(shader_delay=0))
+        ctx.upload_soa(soa)
+        ctx.step(2)
+        frames(2)
+        ctx.export_particles(buf.ptr.value)
+        got = buf.to_host(rps.PARTICLE_DTYPE)
+        assert_bitwise(got["position"][:, 0], ref["x"], "export x")
+        assert_bitwise(got["velocity"][:, 1], ref["vy"], "export vy")
+        ctx.step(2)
+        frames(2)
+        assert_soa_bitwise(ctx.download_soa(), ref, what="after export ")
+        ctx.step(2)
+        frames(2)
+        x_new = (ref["x"][:100] * np.float32(0.5)).astype(F)
+        ctx.upload_field(rps.FIELD_X, x_new)
+        ref["x"][:100] = x_new
+        ctx.step(2)
+        frames(2)
+        assert_soa_bitwise(ctx.download_soa(), ref, what="after field upload ")
+        ctx.step(2)
+        frames(2)
+        cfg = rps.default_particle_config(n, gravity=80.0)
+        ctx.set_config(cfg, rps.make_ext(shader_delay=3))  # frame_count 0: frames 1, 2 gated
+        ctx.step(4)
+        frames(4, gated=2)
+        assert_bitwise(ctx.read_debug(rps.DEBUG_SPATIAL_LOOKUP), st.lookup, "lookup after gated")
+        assert_soa_bitwise(ctx.download_soa(), ref, what="after gated ")
 
 
 @pytest.mark.parametrize("n", [4096, 50000])
