@@ -31,6 +31,14 @@ __device__ __forceinline__ float sqrt_rn_unscaled(float x) {
   return t;
 }
 
+// sqrtf's bits with the unscaled sequence unless a lane of the wave has 0 < x < 2^-96 (two
+// particles closer than ~1e-14: only ever near the origin); call it where the whole wave (or
+// the lanes a ballot should see) is active.
+__device__ __forceinline__ float sqrt_rn_wave(float x) {
+  const bool tiny = x > 0.0f && x < 0x1p-96f;
+  return __builtin_amdgcn_ballot_w64(tiny) ? sqrtf(x) : sqrt_rn_unscaled(x);
+}
+
 // Particle-state layout in HBM.  STREAM mode keeps the state as *tiled SoA*
 // (AoSoA): tiles of kTile particles, each tile holding four contiguous f32 segments
 // [x | y | vx | vy] (128 KiB).  Lanes read 16 contiguous bytes of each field; a workgroup's

@@ -1599,8 +1599,7 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
           // (0 < sq < 2^-96: two particles closer than ~1e-14, only ever near the origin):
           // the same bits as sqrtf (tools/sqrt_check.hip, every input), 2^22 frame
           // 1.2461 -> 1.2358 ms (same box).
-          const bool tiny = sq > 0.0f && sq < 0x1p-96f;
-          const float dist = __builtin_amdgcn_ballot_w64(tiny) ? sqrtf(sq) : sqrt_rn_unscaled(sq);
+          const float dist = sqrt_rn_wave(sq);
           float k1 = 0.0f, k2 = 0.0f;
           if (!(dist >= r)) {
             const float v = r - dist;
@@ -1722,7 +1721,7 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
   const auto load_pd = [&](uint32_t j) { return sl.rec_pd[j]; };
   const auto pressure = [&](const f4& q) {
     const float dx = q[0] - p[0], dy = q[1] - p[1];
-    const float dist = sqrtf(dx * dx + dy * dy);
+    const float dist = sqrt_rn_wave(dx * dx + dy * dy);
     float dirx, diry;
     if (dist > 0.0001f) {
       dirx = dx / dist;
@@ -1755,7 +1754,7 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
   const auto load_pv = [&](uint32_t j) { return sl.rec_pv[j]; };
   const auto viscosity = [&](const f4& q) {
     const float dx = p[0] - q[0], dy = p[1] - q[1];
-    const float dist = sqrtf(dx * dx + dy * dy);
+    const float dist = sqrt_rn_wave(dx * dx + dy * dy);
     float k = 0.0f;
     if (!(dist >= r)) {
       const float v = r * r - dist * dist;
