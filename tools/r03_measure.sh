@@ -4,9 +4,10 @@
 # Each GPU step has its own time limit; the first failure ends the script.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out/r03m
+O=${OUT:-gpurun_out/r03m}
+mkdir -p $O
 export TMPDIR=/tmp
-O=gpurun_out/r03m
+
 step() { local name=$1 t=$2; shift 2; echo "== $name"; timeout -k 10 "$t" "$@" > $O/$name.out 2> $O/$name.err || { echo "$name failed rc=$?"; tail -20 $O/$name.err; exit 1; }; }
 step bench_default 400 python3 bench.py
 step drv20_a 240 python3 bench.py --gpus 1 --steps 20 --warmup 5
