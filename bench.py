@@ -66,6 +66,10 @@ def parse():
                     help="particles of the SPH CPU-baseline sample (oracle, OpenMP)")
     ap.add_argument("--sph-cpu-frames", type=int, default=3)
     ap.add_argument("--no-configs", action="store_true", help="skip the C1/C2 side measurement")
+    ap.add_argument("--sides-first", default="configs",
+                    help="comma list of side runs (configs, sph, allpairs) measured before the headline "
+                         "(default configs: the chip leaves its idle clock state before the timed region; "
+                         "DESIGN.md §6)")
     ap.add_argument("--export-reps", type=int, default=20,
                     help="render-interop export (rps_export_particles) repetitions timed on the headline state; 0: skip")
     ap.add_argument("--allpairs-timeout", type=float, default=240.0,
@@ -492,6 +496,39 @@ def stats_check(d, st_all, st_shard):
     return ref, ok
 
 
+SIDES = ("configs", "sph", "allpairs")
+
+
+def run_sides(rps, args, d, line, keys):
+    """The side measurements `keys`, each under a watchdog: a hung side run must not cost the
+    headline line (when it was measured already), but fails the run."""
+    import threading
+
+    fns = {"configs": (configs_side, not args.no_configs), "sph": (sph_side, args.sph_n > 0),
+           "allpairs": (allpairs, args.allpairs_n > 0)}
+    for key in keys:
+        fn, on = fns[key]
+        if not on:
+            continue
+
+        def _watchdog(key=key):
+            if d.rank == 0:
+                line[key] = {"error": f"watchdog: no result within {args.allpairs_timeout} s"}
+                if "value" in line:
+                    print(json.dumps(line), flush=True)
+            print(f"bench.py: side run '{key}' hung; exiting {WATCHDOG_RC}", file=sys.stderr, flush=True)
+            os._exit(WATCHDOG_RC)
+
+        timer = threading.Timer(args.allpairs_timeout, _watchdog)
+        timer.daemon = True
+        timer.start()
+        try:
+            line[key] = fn(rps, args, d)
+        except Exception as ex:  # report, keep the headline
+            line[key] = {"error": f"{type(ex).__name__}: {ex}"}
+        timer.cancel()
+
+
 def main():
     args = parse()
     launched = "WORLD_SIZE" in os.environ
@@ -502,6 +539,11 @@ def main():
         print(f"bench.py: --gpus {args.gpus} but the launcher started {d.world} rank(s)", file=sys.stderr)
         sys.exit(2)
     rps = load_impl()
+    # Side runs asked for before the headline (their own contexts; the headline's timed work is
+    # the same either way).
+    first = [k for k in args.sides_first.split(",") if k in SIDES]
+    early = {}
+    run_sides(rps, args, d, early, first)
 
     n = args.particles
     cfg, ext = workload(rps, n, d.world)
@@ -579,28 +621,8 @@ def main():
         line["export"] = export
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(rps, args, cfg, ext)
-    sides = [("configs", configs_side, not args.no_configs), ("sph", sph_side, args.sph_n > 0),
-             ("allpairs", allpairs, args.allpairs_n > 0)]
-    for key, fn, on in sides:
-        if not on:
-            continue
-        import threading
-
-        def _watchdog(key=key):  # a hung side run must not cost the headline line, but fails the run
-            if d.rank == 0:
-                line[key] = {"error": f"watchdog: no result within {args.allpairs_timeout} s"}
-                print(json.dumps(line), flush=True)
-            print(f"bench.py: side run '{key}' hung; exiting {WATCHDOG_RC}", file=sys.stderr, flush=True)
-            os._exit(WATCHDOG_RC)
-
-        timer = threading.Timer(args.allpairs_timeout, _watchdog)
-        timer.daemon = True
-        timer.start()
-        try:
-            line[key] = fn(rps, args, d)
-        except Exception as ex:  # report, keep the headline
-            line[key] = {"error": f"{type(ex).__name__}: {ex}"}
-        timer.cancel()
+    line.update(early)
+    run_sides(rps, args, d, line, [k for k in SIDES if k not in first])
     if d.rank == 0:
         print(json.dumps(line), flush=True)
     d.close()
