@@ -130,7 +130,7 @@ def _frames_vs_oracle(rps, orc, n, soa, cfg, frames, cfg_at=None, download_at=No
 
 @pytest.mark.parametrize("n", [16384, 1 << 21])
 def test_sph_resident_state_frames(gpu, orc, monkeypatch, n):
-    """Slot-resident state (DESIGN.md §5.2): after a layout frame the state stays in that
+    """Slot-resident state (DESIGN.md §4): after a layout frame the state stays in that
     frame's storage order and the sim writes the next frame's bin entries.  Consecutive layout
     frames with no download between them (the debug reads translate the sorted lookup's slot
     payloads back to particle indices), a config change between resident frames (stale bin
