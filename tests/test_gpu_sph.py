@@ -359,6 +359,37 @@ def test_sph_spatial_layout_forced(gpu, orc, monkeypatch, case):
     _frames_vs_oracle(rps, orc, n, soa, cfg, 4, cfg_at=cfg_at)
 
 
+@pytest.mark.parametrize("layout", ["0", "2"])
+@pytest.mark.parametrize("case", ["stacked", "tiny", "huge"])
+def test_sph_division_operand_ranges(gpu, orc, monkeypatch, layout, case):
+    """Operand ranges of the sim's pressure direction `delta / distance` (wgsl:304-310) and its
+    sqrt: stacked: columns and rows of particles with equal coordinates and no velocity along
+    them (dx == 0 or dy == 0 exactly: signed-zero quotients); tiny: coordinates 0 < |x| < 2^-60
+    at the origin (tiny numerators; the sqrt's scaled path); huge: x beyond 2^36 (quotients and
+    squares far from 1).  Without (0) and with (2) the spatial layout, every frame bitwise."""
+    rps = gpu
+    monkeypatch.setenv("RPS_SPH_LAYOUT", layout)
+    n = 4096
+    g = np.random.default_rng(43)
+    cfg = rps.default_particle_config(n, gravity=100.0)
+    soa = _blob(n, 42, spread=40.0)
+    if case == "stacked":
+        soa["x"][:2048] = np.round(soa["x"][:2048] / 3.0).astype(F) * F(3.0)
+        soa["vx"][:2048] = F(0.0)
+        soa["y"][1024:3072] = np.round(soa["y"][1024:3072] / 2.0).astype(F) * F(2.0)
+        soa["x"][3072:3200] = F(0.0)
+        soa["vx"][3072:3200] = F(0.0)
+    elif case == "tiny":
+        soa["x"][:64] = g.uniform(-1e-20, 1e-20, 64).astype(F)
+        soa["x"][64:80] = F(0.0)
+        soa["y"][:80] = g.uniform(-2.0, 2.0, 80).astype(F)
+        soa["vx"][:80] = F(0.0)
+    else:
+        soa["x"][:8] = F(1.0e12)
+        soa["vx"][:8] = F(0.0)
+    _frames_vs_oracle(rps, orc, n, soa, cfg, 3)
+
+
 def test_sph_spatial_layout_gated_frames(gpu, orc, monkeypatch):
     """Layout frames after gated ones (SHADER_DELAY 5) and a config change that resets
     frame_count (gated again), at P == N with the layout forced: lookup, offsets, state."""
