@@ -390,6 +390,42 @@ def test_sph_division_operand_ranges(gpu, orc, monkeypatch, layout, case):
     _frames_vs_oracle(rps, orc, n, soa, cfg, 3)
 
 
+# Slider ranges of src/parameter_gui.rs:38-62.
+_GUI_RANGES = dict(fixed_delta_time=(0.0015, 0.015), gravity=(0.0, 1000.0), damping_factor=(0.0, 1.0),
+                   smoothing_radius=(0.0, 30.0), max_energy=(1000.0, 10000.0), target_density=(0.0, 0.1),
+                   pressure_multiplier=(1.0, 100000.0), viscocity_strength=(0.0, 10.0),
+                   near_density_multiplier=(1.0, 10000.0))
+
+
+@pytest.mark.parametrize("layout", ["0", "2"])
+@pytest.mark.parametrize("seed", [0, 1, 2, 3, 4, "edges"])
+def test_sph_random_gui_configs(gpu, orc, monkeypatch, layout, seed):
+    """Configs a user reaches with the reference's sliders (src/parameter_gui.rs:38-62), applied
+    as apply_gui_updates does (norms recomputed, :89-91): five seeded draws over the slider
+    ranges and one at the ends (radius 0 -- infinite norms --, no gravity, full damping, zero
+    target density, maximal pressure); without (0) and with (2) the spatial layout, four frames
+    each bitwise against the oracle, NaN/inf spread included."""
+    rps = gpu
+    monkeypatch.setenv("RPS_SPH_LAYOUT", layout)
+    n = 4096
+    gui = rps.GUIConfig()
+    if seed == "edges":
+        vals = dict(fixed_delta_time=0.015, gravity=0.0, damping_factor=1.0, smoothing_radius=0.0,
+                    max_energy=1000.0, target_density=0.0, pressure_multiplier=100000.0,
+                    viscocity_strength=10.0, near_density_multiplier=10000.0)
+    else:
+        g = np.random.default_rng(1000 + seed)
+        vals = {k: float(np.float32(g.uniform(lo, hi))) for k, (lo, hi) in _GUI_RANGES.items()}
+        vals["smoothing_radius"] = float(np.float32(g.uniform(2.0, 30.0)))  # the bench's cells stay bounded
+    for k, v in vals.items():
+        setattr(gui, k, v)
+    gui.applied_changes = True
+    cfg = rps.default_particle_config(n)
+    rps.apply_gui_updates(cfg, gui)
+    soa = _blob(n, 500 + (7 if seed == "edges" else seed), spread=60.0)
+    _frames_vs_oracle(rps, orc, n, soa, cfg, 4)
+
+
 def test_sph_spatial_layout_gated_frames(gpu, orc, monkeypatch):
     """Layout frames after gated ones (SHADER_DELAY 5) and a config change that resets
     frame_count (gated again), at P == N with the layout forced: lookup, offsets, state."""
