@@ -1932,32 +1932,34 @@ __global__ __launch_bounds__(kBlock) void sph_runs_kernel(SphLayoutArgs a, const
                                                           const uint2* __restrict__ lookup,
                                                           const f4* __restrict__ st, uint32_t n) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-  if (t >= n) return;
-  const uint2 e = lookup[t];
-  const uint32_t prev = t > 0u ? lookup[t - 1u].x : 0xFFFFFFFFu;
+  const uint32_t lane = threadIdx.x & 63u;
+  const bool valid = t < n;  // every lane stays for the wave-wide ballots below
+  const uint2 e = valid ? lookup[t] : make_uint2(0u, 0u);
+  const uint32_t prev = valid && t > 0u ? lookup[t - 1u].x : 0xFFFFFFFFu;
   const uint32_t next = t + 1u < n ? lookup[t + 1u].x : ~e.x;
-  if (next != e.x) a.run_end[e.x] = t + 1u;
-  if (e.x == prev) return;
+  if (valid && next != e.x) a.run_end[e.x] = t + 1u;
+  const bool start = valid && e.x != prev;
+  // Run lengths without a walk: a run starting in this wave ends at the wave's next run start
+  // or, for the wave's last run, where the 64 slots after the wave first hold another key (one
+  // coalesced load per lane; a run reaching past them is longer than kRunScan, so listed).
+  const uint64_t starts = __builtin_amdgcn_ballot_w64(start);
+  const uint32_t klast = (uint32_t)__builtin_amdgcn_readlane((int)e.x, 63);
+  const uint32_t u = t + 64u;  // slot lane of the 64 after the wave
+  const bool same = u < n && lookup[u].x == klast;
+  const uint64_t other = __builtin_amdgcn_ballot_w64(!same);
+  if (!start) return;
+  const uint64_t above = lane == 63u ? 0ull : starts >> (lane + 1u);
+  const uint32_t len = above ? (uint32_t)__builtin_ctzll(above) + 1u
+                             : min(64u - lane, n - t) + (other ? (uint32_t)__builtin_ctzll(other) : 64u);
   // The cell of the run's first particle, computed as the bin pass did (same state, same
   // ops), so its key is e.x; anything else (never seen) is handled as outside the grid.
   const f4 s = st[e.y];
-  // Length, and the first kRunIdx particle indices (the write pass then needs no lookup
-  // gathers for them).
-  // The next entries are loaded together (adjacent, mostly one line), then measured.
-  uint2 nx[kRunIdx];
-#pragma unroll
-  for (uint32_t k = 1; k < kRunIdx; ++k) nx[k] = t + k < n ? lookup[t + k] : make_uint2(~e.x, 0u);
+  // The first kRunIdx particle indices (the write pass then needs no lookup gathers for
+  // them), loaded together (adjacent, mostly one line).
   uint32_t idx[kRunIdx];
   idx[0] = e.y;
-  uint32_t len = 1;
 #pragma unroll
-  for (uint32_t k = 1; k < kRunIdx; ++k) {
-    const bool more = len == k && nx[k].x == e.x;
-    idx[k] = more ? nx[k].y : 0u;
-    len = more ? k + 1u : len;
-  }
-  if (len == kRunIdx)
-    while (len <= kRunScan && t + len < n && lookup[t + len].x == e.x) ++len;
+  for (uint32_t k = 1; k < kRunIdx; ++k) idx[k] = k < len ? lookup[t + k].y : 0u;
   const float r = cfg->smoothing_radius;
   const int32_t cx = f32_to_i32((s[0] + cfg->screen_bounds[1]) / r);
   const int32_t cy = f32_to_i32((s[1] + cfg->screen_bounds[3]) / r);
