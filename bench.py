@@ -72,6 +72,8 @@ def parse():
                          "DESIGN.md §6)")
     ap.add_argument("--export-reps", type=int, default=20,
                     help="render-interop export (rps_export_particles) repetitions timed on the headline state; 0: skip")
+    ap.add_argument("--export-after", action="store_true",
+                    help="measure the export after the headline's timed region instead of before its warmup")
     ap.add_argument("--allpairs-timeout", type=float, default=240.0,
                     help="watchdog: print the headline line and exit non-zero if a side run hangs")
     ap.add_argument("--master-port", type=int, default=0,
@@ -554,6 +556,10 @@ def main():
     if d.dist:  # under a launcher the stats steps all-reduce over the ranks inside librps (RCCL)
         ctx.comm_init(d.rank, d.world, d.broadcast_bytes(rps.comm_unique_id() if d.rank == 0 else b""))
     ctx.init_scatter(args.seed)
+    do_export = args.export_reps > 0 and hasattr(ctx, "stream_ptr")
+    export = None
+    if do_export and not args.export_after:  # reads the state only: the headline's work is unchanged
+        export = export_side(ctx, n, args.export_reps)
     ctx.step(args.warmup)
     ctx.sync()
 
@@ -574,7 +580,8 @@ def main():
     launches = args.steps
     moved_per_launch, _ = ctx.step_cost()  # bytes the kernel moves: 32.03 B per particle
     algo_per_launch = ALGO_BYTES_PER_PARTICLE * n
-    export = export_side(ctx, n, args.export_reps) if args.export_reps > 0 and hasattr(ctx, "stream_ptr") else None
+    if do_export and args.export_after:
+        export = export_side(ctx, n, args.export_reps)
     if d.dist:
         stats, stats_ok = stats_check(d, ctx.stats(), ctx.shard_stats())
     else:
