@@ -426,6 +426,17 @@ def test_sph_random_gui_configs(gpu, orc, monkeypatch, layout, seed):
     _frames_vs_oracle(rps, orc, n, soa, cfg, 4)
 
 
+@pytest.mark.parametrize("n", [1, 2, 16, 64, 128, 1024])
+def test_sph_spatial_layout_small_n(gpu, orc, monkeypatch, n):
+    """The layout forced at power-of-two N below and around one wave (the runs kernel sizes a
+    run from the wave's run-start ballot and one look-ahead load past the wave; lanes past N
+    take part in the ballots): four frames bitwise."""
+    rps = gpu
+    monkeypatch.setenv("RPS_SPH_LAYOUT", "2")
+    cfg = rps.default_particle_config(n, gravity=100.0)
+    _frames_vs_oracle(rps, orc, n, _blob(n, 70 + n, spread=15.0), cfg, 4)
+
+
 def test_sph_spatial_layout_gated_frames(gpu, orc, monkeypatch):
     """Layout frames after gated ones (SHADER_DELAY 5) and a config change that resets
     frame_count (gated again), at P == N with the layout forced: lookup, offsets, state."""
