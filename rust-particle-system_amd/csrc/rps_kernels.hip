@@ -1346,7 +1346,8 @@ __global__ __launch_bounds__(kBlock) void sph_offsets_kernel(const uint2* __rest
   if (key != next || i + 1u == n) ends[key] = i + 1u;
 }
 
-// Spatial record layout: cell enumeration (8 x 8 tiles; see the layout kernels below).
+// Spatial record layout: cell enumeration (8 x 8 tiles; see the layout kernels below; tall
+// tiles measured equal).
 constexpr uint32_t kCellOut = 0xFFFFFFFFu;
 constexpr uint32_t kCellPending = 0xFFFFFFFEu;  // cellrun entry to resolve through run2
 constexpr uint32_t kRunScan = 32u;               // longest run a runs-kernel lane measures itself
@@ -1355,7 +1356,15 @@ constexpr uint32_t kRunIdx = 6u;                 // particle indices a run's cel
 #ifndef RPS_CELL_TILE_LOG
 #define RPS_CELL_TILE_LOG 3  // 8 x 8 cells per tile (4 x 4: equal, 16 x 16: slower)
 #endif
-constexpr uint32_t kCT = RPS_CELL_TILE_LOG, kCTM = (1u << kCT) - 1u;
+#ifndef RPS_CELL_TILE_LOG_X
+#define RPS_CELL_TILE_LOG_X RPS_CELL_TILE_LOG
+#endif
+#ifndef RPS_CELL_TILE_LOG_Y
+#define RPS_CELL_TILE_LOG_Y RPS_CELL_TILE_LOG
+#endif
+// Tile width 2^kCX and height 2^kCY cells.
+constexpr uint32_t kCX = RPS_CELL_TILE_LOG_X, kCY = RPS_CELL_TILE_LOG_Y;
+constexpr uint32_t kCXM = (1u << kCX) - 1u, kCYM = (1u << kCY) - 1u, kCXY = kCX + kCY;
 #ifndef RPS_TILE_COLMAJOR
 #define RPS_TILE_COLMAJOR 0  // tiles column by column (slower, below)
 #endif
@@ -1366,12 +1375,12 @@ constexpr uint32_t kCT = RPS_CELL_TILE_LOG, kCTM = (1u << kCT) - 1u;
 #define RPS_CELL_COLMAJOR 1
 #endif
 __device__ __forceinline__ uint32_t grid_enum_xy(const SphGrid& g, uint32_t x, uint32_t y) {
-  const uint32_t in_tile = RPS_CELL_COLMAJOR ? (((x & kCTM) << kCT) | (y & kCTM)) : (((y & kCTM) << kCT) | (x & kCTM));
+  const uint32_t in_tile = RPS_CELL_COLMAJOR ? (((x & kCXM) << kCY) | (y & kCYM)) : (((y & kCYM) << kCX) | (x & kCXM));
 #if RPS_TILE_COLMAJOR
-  const uint32_t th = (g.cells >> (2u * kCT)) / g.tw;
-  return (((x >> kCT) * th + (y >> kCT)) << (2u * kCT)) | in_tile;
+  const uint32_t th = (g.cells >> kCXY) / g.tw;
+  return (((x >> kCX) * th + (y >> kCY)) << kCXY) | in_tile;
 #else
-  return (((y >> kCT) * g.tw + (x >> kCT)) << (2u * kCT)) | in_tile;
+  return (((y >> kCY) * g.tw + (x >> kCX)) << kCXY) | in_tile;
 #endif
 }
 __device__ __forceinline__ uint32_t grid_enum(const SphGrid& g, int32_t cx, int32_t cy) {
@@ -1382,17 +1391,17 @@ __device__ __forceinline__ uint32_t grid_enum(const SphGrid& g, int32_t cx, int3
 
 // Inverse of grid_enum; false for the padding cells of edge tiles.
 __device__ __forceinline__ bool grid_cell(const SphGrid& g, uint32_t e, int32_t& cx, int32_t& cy) {
-  const uint32_t tile = e >> (2u * kCT);
+  const uint32_t tile = e >> kCXY;
 #if RPS_TILE_COLMAJOR
-  const uint32_t th = (g.cells >> (2u * kCT)) / g.tw;
+  const uint32_t th = (g.cells >> kCXY) / g.tw;
   const uint32_t tx_ = tile / th, ty = tile - tx_ * th;
   const uint32_t tile_rm = ty * g.tw + tx_;  // the same tile in row-major numbering
 #else
   const uint32_t ty = tile / g.tw, tile_rm = tile;
 #endif
-  const uint32_t lo = RPS_CELL_COLMAJOR ? ((e >> kCT) & kCTM) : (e & kCTM);
-  const uint32_t hi = RPS_CELL_COLMAJOR ? (e & kCTM) : ((e >> kCT) & kCTM);
-  const uint32_t x = ((tile_rm - ty * g.tw) << kCT) + lo, y = (ty << kCT) + hi;
+  const uint32_t lo = RPS_CELL_COLMAJOR ? ((e >> kCY) & kCXM) : (e & kCXM);
+  const uint32_t hi = RPS_CELL_COLMAJOR ? (e & kCYM) : ((e >> kCX) & kCYM);
+  const uint32_t x = ((tile_rm - ty * g.tw) << kCX) + lo, y = (ty << kCY) + hi;
   cx = (int32_t)((uint32_t)g.cx_lo + x);
   cy = (int32_t)((uint32_t)g.cy_lo + y);
   return x < g.w && y < g.h;
@@ -2461,15 +2470,15 @@ bool sph_layout_grid(const rps_config& c, uint32_t cell_cap, SphGrid* g) {
   const double y1 = std::floor(((double)c.screen_bounds[3] + c.screen_bounds[3]) / r) + 1.0;
   if (!(x1 >= x0) || !(y1 >= y0) || x0 < -2.0e9 || y0 < -2.0e9 || x1 > 2.0e9 || y1 > 2.0e9) return false;
   const double w = x1 - x0 + 1.0, h = y1 - y0 + 1.0;
-  const double ts = (double)(1u << kCT);
-  const double tw = std::ceil(w / ts), th = std::ceil(h / ts);
-  if (tw * th * ts * ts > (double)cell_cap) return false;
+  const double tsx = (double)(1u << kCX), tsy = (double)(1u << kCY);
+  const double tw = std::ceil(w / tsx), th = std::ceil(h / tsy);
+  if (tw * th * tsx * tsy > (double)cell_cap) return false;
   g->cx_lo = (int32_t)x0;
   g->cy_lo = (int32_t)y0;
   g->w = (uint32_t)w;
   g->h = (uint32_t)h;
   g->tw = (uint32_t)tw;
-  g->cells = (uint32_t)(tw * th * ts * ts);
+  g->cells = (uint32_t)(tw * th * tsx * tsy);
   return true;
 }
 
