@@ -942,10 +942,13 @@ int rps_read_debug(rps_ctx* ctx, int which, void* dst, uint64_t bytes) {
                                              ctx->stream));
     src = ctx->lay.out_runs;
   }
-  // A spatial-layout frame measures its runs without writing the reference's offsets (the bin
-  // pass reset them): pass 3 (wgsl:507-525) on the frame's sorted lookup, on demand.
-  if (which == RPS_DEBUG_LOOKUP_OFFSETS && ctx->layout_last)
+  // A spatial-layout frame measures its runs without touching the reference's offsets:
+  // bin_particles_in_grid's reset (wgsl:467) and pass 3 (wgsl:507-525) on the frame's sorted
+  // lookup, on demand.
+  if (which == RPS_DEBUG_LOOKUP_OFFSETS && ctx->layout_last) {
+    RPS_HIP(ctx, hipMemsetAsync(ctx->offsets, 0xFF, ctx->n * sizeof(uint32_t), ctx->stream));
     RPS_HIP(ctx, launch_sph_offsets(sph_buffers(ctx), ctx->stream));
+  }
   RPS_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
   RPS_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return RPS_OK;

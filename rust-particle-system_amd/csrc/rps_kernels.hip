@@ -1192,10 +1192,8 @@ __device__ __forceinline__ void bin_keys(const SortBin& bin, uint32_t base0, uin
     const uint32_t q = t + k * NT, gq = base0 + q;
     if (gq >= bin.n) {
       s[q] = raw[k];
-    } else if (bin.prebuilt) {  // (key, slot): the resets of bin_key only
-      bin.offsets[gq] = 0xFFFFFFFFu;
-      if (bin.run2) bin.run2[gq] = make_uint2(0xFFFFFFFFu, 0u);
-      s[q] = raw[k];
+    } else if (bin.prebuilt) {  // (key, slot) of a layout frame: run2 is reset by the runs kernel,
+      s[q] = raw[k];             // offsets on debug readback (rps_read_debug)
     } else {
       s[q] = bin_key(bin, __builtin_bit_cast(f2, raw[k]), gq);
     }
@@ -1947,6 +1945,7 @@ __global__ __launch_bounds__(kBlock) void sph_runs_kernel(SphLayoutArgs a, const
   const uint32_t prev = valid && t > 0u ? lookup[t - 1u].x : 0xFFFFFFFFu;
   const uint32_t next = t + 1u < n ? lookup[t + 1u].x : ~e.x;
   if (valid && next != e.x) a.run_end[e.x] = t + 1u;
+  if (valid) a.run2[t] = make_uint2(0xFFFFFFFFu, 0u);  // no run for key t until the scan / write kernels
   const bool start = valid && e.x != prev;
   // Run lengths without a walk: a run starting in this wave ends at the wave's next run start
   // or, for the wave's last run, where the 64 slots after the wave first hold another key (one
