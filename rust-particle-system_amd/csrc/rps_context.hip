@@ -625,11 +625,12 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     slots.push_back({(void**)&ctx->dens, align_up(n * sizeof(f2), 256)});
     slots.push_back({(void**)&ctx->pred, align_up(n * sizeof(f2), 256)});
     slots.push_back({(void**)&ctx->d_count, align_up(2 * sph_count_blocks(ctx->P) * sizeof(unsigned long long), 256)});
-    // Spatial record layout (rps_kernels.hip): RPS_SPH_LAYOUT=0 off, 1 (default) from 2^21
-    // particles, where it is measured faster (2^22 frame 1.212 -> 1.121 ms, 2^21 0.633 ->
-    // 0.609; 2^20 0.385 -> 0.391 and 2^18 0.166 -> 0.176 slower: DESIGN.md §5), 2 at any P == N.
+    // Spatial record layout (rps_kernels.hip): RPS_SPH_LAYOUT=0 off, 1 (default) from 2^20
+    // particles, where it is measured faster (with slot-resident state, same box: 2^20 frame
+    // 0.3442 -> 0.3230 ms, 2^19 0.2274 -> 0.2269, 2^18 0.1429 -> 0.1458 slower),
+    // 2 at any P == N.
     const int lay_mode = env_int("RPS_SPH_LAYOUT", 1);
-    if (P == n && (lay_mode == 2 || (lay_mode == 1 && n >= (1u << 21)))) {
+    if (P == n && (lay_mode == 2 || (lay_mode == 1 && n >= (1u << 20)))) {
       // Up to 1 cell per particle (the bench's viewport, like the reference default, has
       // ~0.52), and at least the reference's default 1920 x 1080 viewport (~27 000 cells).
       ctx->cell_cap = (uint32_t)std::max<size_t>(n, 1u << 16);

@@ -251,11 +251,11 @@ def test_sph_forced_scan_batches(gpu, orc, monkeypatch, n, batch):
     _frames_vs_oracle(rps, orc, n, _blob(n, n + 2), cfg, 3)
 
 
-@pytest.mark.parametrize("n", [1 << 22, 1 << 21])
+@pytest.mark.parametrize("n", [1 << 22, 1 << 21, 1 << 20])
 def test_sph_bench_workload_full_size(gpu, orc, n):
     """The bench's `sph` workload exactly (2^22): particles of the reference scatter over a
-    viewport scaled to the default density, every frame active.  Both sizes run the spatial
-    record layout (from 2^21) with its 4-entry sim scan; P = 2^22 selects 8192-entry sort
+    viewport scaled to the default density, every frame active.  Every size runs the spatial
+    record layout (from 2^20) with its 4-entry sim scan; P = 2^22 selects 8192-entry sort
     tiles with 3 passes per register chunk and the five-pass register-fused global stage; at
     P = 2^21 that stage is a gathered-tile launch.  Two frames, every pass bitwise."""
     rps = gpu
