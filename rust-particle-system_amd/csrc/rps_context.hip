@@ -28,6 +28,7 @@ struct rps_ctx {
   uint32_t mode = RPS_MODE_STREAM;
   uint64_t n = 0, id_offset = 0, global_count = 0;
   hipStream_t stream = nullptr;
+  hipEvent_t ev_begin = nullptr, ev_end = nullptr;  // rps_time_steps (created with the stream)
 
   rps_config cfg{};
   rps_ext_config ext{};
@@ -589,6 +590,10 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     ctx->err = "hipStreamCreate failed";
     return bail(RPS_ERR_DEVICE);
   }
+  if (hipEventCreate(&ctx->ev_begin) != hipSuccess || hipEventCreate(&ctx->ev_end) != hipSuccess) {
+    ctx->err = "hipEventCreate failed";
+    return bail(RPS_ERR_DEVICE);
+  }
 
   // Carve the arena: every array 256-B aligned (16-B vector access + full cache lines).
   const size_t n = ctx->n;
@@ -716,6 +721,8 @@ int rps_destroy(rps_ctx* ctx) {
   if (ctx->nb_stamps) (void)hipFree(ctx->nb_stamps);
   if (ctx->partials) (void)hipFree(ctx->partials);
   if (ctx->arena) (void)hipFree(ctx->arena);
+  if (ctx->ev_begin) (void)hipEventDestroy(ctx->ev_begin);
+  if (ctx->ev_end) (void)hipEventDestroy(ctx->ev_end);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return RPS_OK;
@@ -1160,20 +1167,17 @@ int rps_get_kernel_times(rps_ctx* ctx, double* ms, uint64_t cap, uint64_t* launc
 int rps_time_steps(rps_ctx* ctx, uint32_t nsteps, double* total_ms) {
   int rc = check_ctx(ctx);
   if (rc) return rc;
-  hipEvent_t a, b;
-  RPS_HIP(ctx, hipEventCreate(&a));
-  RPS_HIP(ctx, hipEventCreate(&b));
-  RPS_HIP(ctx, hipEventRecord(a, ctx->stream));
+  // The context's two events (created with its stream, so no allocation between the caller's
+  // clock and the first launch).
+  RPS_HIP(ctx, hipEventRecord(ctx->ev_begin, ctx->stream));
   rc = rps_step(ctx, nsteps);
   if (rc == RPS_OK) {
-    RPS_HIP(ctx, hipEventRecord(b, ctx->stream));
-    RPS_HIP(ctx, hipEventSynchronize(b));
+    RPS_HIP(ctx, hipEventRecord(ctx->ev_end, ctx->stream));
+    RPS_HIP(ctx, hipEventSynchronize(ctx->ev_end));
     float ms = 0.0f;
-    RPS_HIP(ctx, hipEventElapsedTime(&ms, a, b));
+    RPS_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev_begin, ctx->ev_end));
     if (total_ms) *total_ms = ms;
   }
-  (void)hipEventDestroy(a);
-  (void)hipEventDestroy(b);
   return rc;
 }
 
