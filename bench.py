@@ -382,7 +382,7 @@ def sph_side(rps, args, d):
     hbm_frame = (pmc or {}).get("frame_sum_of_kernels", {}).get("hbm_bytes")
     pow2 = n & (n - 1) == 0
     layout = os.environ.get("RPS_SPH_LAYOUT", "1")
-    spatial = pow2 and (layout == "2" or (layout == "1" and n >= (1 << 21)))  # rps_context.hip
+    spatial = pow2 and (layout == "2" or (layout == "1" and n >= (1 << 20)))  # rps_context.hip
     out = {"workload": f"SPH frame (5 passes, bitwise == oracle), {n} particles per rank, reference scatter",
            "record_layout": "cell tiles (spatial)" if spatial else "lookup order",
            "scaling": "replicas", "frames": args.sph_frames, "ms_per_frame": frame_ms,

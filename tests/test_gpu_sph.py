@@ -331,7 +331,7 @@ def test_sph_frame_cost_counts(gpu, orc, monkeypatch, n, layout):
 
 @pytest.mark.parametrize("case", ["blob", "dense", "outside", "batches"])
 def test_sph_spatial_layout_forced(gpu, orc, monkeypatch, case):
-    """The spatial record layout (rps_kernels.hip; by default only from 2^21 particles) forced
+    """The spatial record layout (rps_kernels.hip; by default only from 2^20 particles) forced
     at small P == N, every pass bitwise: an ordinary blob; a dense one whose runs exceed the
     runs kernel's 32-entry measure (the listed-run path); particles far outside the walls
     (runs owned by cells beyond the grid, lanes whose 3 x 3 block leaves it) with a radius +
@@ -471,8 +471,8 @@ def test_sph_layout_clustered_runs(gpu, orc, monkeypatch):
     """Runs longer than the layout's 32-entry measure (a clump of particles in one cell) are
     'listed' by the runs kernel.  Their lengths come from the per-key run ends and their slots'
     prediction is spread over every thread of the write kernel (round 2 walked and predicted
-    each listed run on one lane, O(run length) dependent loads).  At 2^21 (the layout's default
-    from there on) with 16 clumps of 4096 particles each inside one cell: the first frame
+    each listed run on one lane, O(run length) dependent loads).  At 2^21 (where the layout is the default
+    ) with 16 clumps of 4096 particles each inside one cell: the first frame
     bitwise against the oracle, and the layout frame no slower than 1.5x the lookup-order
     frame of the same state (same clumps, same scans; only the record placement differs)."""
     rps = gpu
