@@ -471,8 +471,8 @@ def test_sph_layout_clustered_runs(gpu, orc, monkeypatch):
     """Runs longer than the layout's 32-entry measure (a clump of particles in one cell) are
     'listed' by the runs kernel.  Their lengths come from the per-key run ends and their slots'
     prediction is spread over every thread of the write kernel (round 2 walked and predicted
-    each listed run on one lane, O(run length) dependent loads).  At 2^21 (where the layout is the default
-    ) with 16 clumps of 4096 particles each inside one cell: the first frame
+    each listed run on one lane, O(run length) dependent loads).  At 2^21 (a default layout
+    size) with 16 clumps of 4096 particles each inside one cell: the first frame
     bitwise against the oracle, and the layout frame no slower than 1.5x the lookup-order
     frame of the same state (same clumps, same scans; only the record placement differs)."""
     rps = gpu
