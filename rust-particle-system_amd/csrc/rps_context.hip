@@ -625,6 +625,7 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     slots.push_back({(void**)&ctx->sl.cur_s, align_up(P * sizeof(f2), 256)});
     slots.push_back({(void**)&ctx->ends, align_up(n * sizeof(uint32_t), 256)});
     slots.push_back({(void**)&ctx->sl.nbr_mask, align_up(2 * P * sizeof(uint64_t), 256)});
+    if (P != n) slots.push_back({(void**)&ctx->sl.owner, align_up(n * sizeof(uint32_t), 256)});
     slots.push_back({(void**)&ctx->lookup, align_up((size_t)ctx->P * sizeof(uint2), 256)});
     slots.push_back({(void**)&ctx->offsets, align_up(n * sizeof(uint32_t), 256)});
     slots.push_back({(void**)&ctx->dens, align_up(n * sizeof(f2), 256)});

@@ -107,6 +107,11 @@ struct SphSlots {
   uint32_t* idx_s;  // P particle index (self-skip, wgsl:295 / :365)
   f2* cur_s;     // P current positions (Euler base)
   uint64_t* nbr_mask;  // 2 x P: bit f set <=> flat entry f of the nine runs is within the radius
+  // P != N only (else nullptr): owner[i] = the lowest slot holding particle i in the last active
+  // frame (reset before its predict pass, claimed by atomicMin in it).  Pad
+  // slots repeat particles; a repeat computes exactly its owner's values, so the
+  // sim runs on owner slots only, and slots >= N (never a neighbour entry) skip the density too.
+  uint32_t* owner;
 };
 // Cell range of the spatial record layout (rps_kernels.hip): cells [cx_lo, cx_lo + w) x
 // [cy_lo, cy_lo + h), enumerated in 8 x 8 tiles, tw tiles per row; cells = tiles x 64.

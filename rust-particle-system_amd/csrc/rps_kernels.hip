@@ -1450,6 +1450,7 @@ __global__ __launch_bounds__(kBlock) void sph_predict_kernel(const rps_config* _
     if (e.x != prev) offsets[e.x] = t;
     if (e.x != next || t + 1u == n_offsets) ends[e.x] = t + 1u;
   }
+  if (sl.owner) atomicMin(&sl.owner[e.y], t);
   predict_slot(cfg, st, sl, t, e.y);
 }
 
@@ -1577,9 +1578,10 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
                                                              RunBounds rb, SphSlots sl, uint32_t p_slots) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= p_slots) return;
+  const uint32_t N = cfg->particle_count;
+  if (sl.owner && t >= N && sl.owner[sl.idx_s[t]] != t) return;  // a repeat no scan visits
   const f2 p = sl.pp_s[t];
   const float r = cfg->smoothing_radius, r2 = r * r;
-  const uint32_t N = cfg->particle_count;
   const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
   __shared__ RunTable runs;
   const uint32_t total = nine_runs<LAYOUT>(rb, p[0], p[1], cfg->screen_bounds[1],
@@ -1708,6 +1710,7 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
   const f4 own = sl.rec_pd[t];  // own predicted position (xy) and P / rho^2 (z)
   const f2 own_d = sl.dens_s[t];
   const uint32_t i = sl.idx_s[t];
+  if (kPads && sl.owner[i] != t) return;  // a repeat: its owner slot computes the same state
   const uint32_t self = kPads ? i : t;
   const float dt = cfg->fixed_delta_time;
   const float r = cfg->smoothing_radius, r2 = r * r;
@@ -1802,6 +1805,7 @@ __global__ __launch_bounds__(kBlock) void sph_debug_views_kernel(SphSlots sl, f2
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= p_slots) return;
   const uint32_t i = sl.idx_s[t];
+  if (sl.owner && sl.owner[i] != t) return;  // repeats may have skipped the density pass
   pred[i] = sl.pp_s[t];
   dens[i] = sl.dens_s[t];
 }
@@ -2452,6 +2456,12 @@ static hipError_t launch_sph_density(const SphBuffers& b, hipStream_t s) {
 }
 
 hipError_t launch_sph_pre(const SphBuffers& b, hipStream_t s) {
+  // Owners are claimed by the predict pass of active frames only, so after gated frames they
+  // still describe the slot records (rps_read_debug's views).
+  if (b.sl.owner) {
+    const hipError_t e = hipMemsetAsync(b.sl.owner, 0xFF, (size_t)b.n * sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(sph_predict_kernel, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg, b.lookup, b.st,
                      b.sl, b.p, b.offsets, b.ends, b.n);
   const hipError_t e = hipGetLastError();
