@@ -1589,7 +1589,13 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
   RunCursor rc(runs);
   float d = 0.0f, nd = 0.0f;
   uint64_t m0 = 0, m1 = 0;
-  for (uint32_t f = 0; f < total; f += kScanBatch) {
+  // Density and near density both NaN stay NaN whatever is added (payloads aside, DESIGN.md
+  // §3.4).  With the particle's own position finite, the entry that made them NaN is another
+  // particle's NaN (or infinite) position, already in the mask, and the sim's pressure term for
+  // it is NaN in both components: the particle's state ends NaN whatever follows, so the scan
+  // stops there (the rest of the mask unset).  An own non-finite position scans everything.
+  const bool own_finite = fabsf(p[0]) < INFINITY && fabsf(p[1]) < INFINITY;
+  for (uint32_t f = 0; f < total && !(own_finite && d != d && nd != nd); f += kScanBatch) {
     f2 q[kScanBatch];
 #pragma unroll
     for (int u = 0; u < kScanBatch; ++u) q[u] = sl.pp_s[rc.slot(min(f + u, total - 1u))];
@@ -1637,11 +1643,12 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
 // :365) compares particle indices; with P == N there are no pad entries, every particle owns
 // exactly one slot, and the index test is the slot test j != t, which saves the 4-B index
 // load per entry (kPads = false).
-template <int kScanBatch, bool kPads, class Load, class Body>
+template <int kScanBatch, bool kPads, class Load, class Body, class Done>
 __device__ __forceinline__ void scan_masked(const SphSlots& sl, const RunTable& runs, uint64_t m0,
-                                            uint64_t m1, uint32_t self, Load&& load, Body&& body) {
+                                            uint64_t m1, uint32_t self, Load&& load, Body&& body,
+                                            Done&& done) {
   RunCursor rc(runs);
-  while (m0 | m1) {
+  while ((m0 | m1) && !done()) {
     uint32_t fs[kScanBatch], qi[kScanBatch];
     bool live[kScanBatch];
     f4 q[kScanBatch];
@@ -1670,12 +1677,12 @@ __device__ __forceinline__ void scan_masked(const SphSlots& sl, const RunTable& 
   }
 }
 
-template <int kScanBatch, bool kPads, class Load, class Body>
+template <int kScanBatch, bool kPads, class Load, class Body, class Done>
 __device__ __forceinline__ void scan_runs(const SphSlots& sl, const RunTable& runs, uint32_t f0,
                                           uint32_t total, f2 p, float r2, uint32_t self, Load&& load,
-                                          Body&& body) {
+                                          Body&& body, Done&& done) {
   RunCursor rc(runs);
-  for (uint32_t f = f0; f < total; f += kScanBatch) {
+  for (uint32_t f = f0; f < total && !done(); f += kScanBatch) {
     f4 q[kScanBatch];
     uint32_t qi[kScanBatch];
 #pragma unroll
@@ -1753,10 +1760,13 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
     fx = fx + (dirx * npt) * ndk;
     fy = fy + (diry * npt) * ndk;
   };
+  // A force sum that is NaN in both components stays NaN whatever is added (payloads aside,
+  // DESIGN.md §3.4): the scan stops there.  Only a particle whose state ends NaN gets there.
+  const auto pressure_nan = [&] { return fx != fx && fy != fy; };
   if (masked)
-    scan_masked<kScanBatch, kPads>(sl, runs, m0, m1, self, load_pd, pressure);
+    scan_masked<kScanBatch, kPads>(sl, runs, m0, m1, self, load_pd, pressure, pressure_nan);
   else
-    scan_runs<kScanBatch, kPads>(sl, runs, 0u, total, p, r2, self, load_pd, pressure);
+    scan_runs<kScanBatch, kPads>(sl, runs, 0u, total, p, r2, self, load_pd, pressure, pressure_nan);
   const f4 own_pv = sl.rec_pv[t];
   float qx = own_pv[2] + fx * dt;  // post-gravity velocity (the pre pass, wgsl:397-400)
   float qy = own_pv[3] + fy * dt;
@@ -1773,10 +1783,11 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
     wx = wx + (q[2] - qx) * k;
     wy = wy + (q[3] - qy) * k;
   };
+  const auto viscosity_nan = [&] { return wx != wx && wy != wy; };
   if (masked)
-    scan_masked<kScanBatch, kPads>(sl, runs, m0, m1, self, load_pv, viscosity);
+    scan_masked<kScanBatch, kPads>(sl, runs, m0, m1, self, load_pv, viscosity, viscosity_nan);
   else
-    scan_runs<kScanBatch, kPads>(sl, runs, 0u, total, p, r2, self, load_pv, viscosity);
+    scan_runs<kScanBatch, kPads>(sl, runs, 0u, total, p, r2, self, load_pv, viscosity, viscosity_nan);
   qx = qx + (wx * cfg->viscocity_strength) * dt;
   qy = qy + (wy * cfg->viscocity_strength) * dt;
   const f2 c = sl.cur_s[t];

@@ -437,6 +437,25 @@ def test_sph_spatial_layout_small_n(gpu, orc, monkeypatch, n):
     _frames_vs_oracle(rps, orc, n, _blob(n, 70 + n, spread=15.0), cfg, 4)
 
 
+@pytest.mark.parametrize("layout", ["0", "2"])
+def test_sph_nan_and_inf_uploads(gpu, orc, monkeypatch, layout):
+    """Uploaded non-finite state: NaN positions with finite velocities, infinite positions, NaN
+    velocities, amid ordinary particles.  The scans stop a sum once it is NaN in every component
+     only where the particle's state ends NaN anyway; a particle whose own
+    position is not finite scans everything.  Every frame bitwise (any NaN equals any NaN)."""
+    rps = gpu
+    monkeypatch.setenv("RPS_SPH_LAYOUT", layout)
+    n = 4096
+    cfg = rps.default_particle_config(n, gravity=100.0)
+    soa = _blob(n, 91, spread=150.0)  # NaN spreads to ~330 particles in 4 frames
+    soa["x"][:6] = F(np.nan)
+    soa["y"][6:9] = F(np.nan)
+    soa["x"][9:12] = F(np.inf)
+    soa["y"][12:14] = F(-np.inf)
+    soa["vx"][14:20] = F(np.nan)
+    _frames_vs_oracle(rps, orc, n, soa, cfg, 4)
+
+
 def test_sph_spatial_layout_gated_frames(gpu, orc, monkeypatch):
     """Layout frames after gated ones (SHADER_DELAY 5) and a config change that resets
     frame_count (gated again), at P == N with the layout forced: lookup, offsets, state."""
