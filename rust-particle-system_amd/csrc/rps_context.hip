@@ -646,6 +646,7 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
       slots.push_back({(void**)&ctx->lay.run2, align_up(n * sizeof(uint2), 256)});
       slots.push_back({(void**)&ctx->lay.part, align_up((cap / 256 + 2) * sizeof(uint32_t), 256)});
       slots.push_back({(void**)&ctx->lay.out_runs, align_up(n * sizeof(uint2), 256)});
+      slots.push_back({(void**)&ctx->lay.keybits, align_up((n / 32 + 1) * sizeof(uint32_t), 256)});
       slots.push_back({(void**)&ctx->lay.n_out, 256});
       slots.push_back({(void**)&ctx->st_alt, align_up(n * sizeof(f4), 256)});
       slots.push_back({(void**)&ctx->idx_alt, align_up(P * sizeof(uint32_t), 256)});

@@ -130,6 +130,8 @@ struct SphLayoutArgs {
   uint2* out_runs;     // N: {first slot, storage base} of the runs placed after the grid's
   uint32_t* n_out;     // 1: their count (0 between frames)
   uint32_t* run_end;   // N: one past the last slot of each key's run (the runs kernel)
+  uint32_t* keybits;   // N / 32: bit k set <=> key k has a run this frame (set by the runs
+                       //   kernel, read by fixup, cleared by the density pass)
 };
 struct SphBuffers {
   const rps_config* cfg;  // device-resident ParticleConfig

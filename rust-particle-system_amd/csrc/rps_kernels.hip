@@ -1476,6 +1476,7 @@ struct RunBounds {
   const uint2* cellrun;
   const uint2* run2;
   SphGrid g;
+  uint32_t* keybits;  // SphLayoutArgs::keybits (the density pass clears it for the next frame)
 };
 
 template <bool LAYOUT>
@@ -1579,6 +1580,7 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= p_slots) return;
   const uint32_t N = cfg->particle_count;
+  if (LAYOUT && t <= N / 32u) rb.keybits[t] = 0u;  // the fixup has read it; the next runs kernel sets it
   if (sl.owner && t >= N && sl.owner[sl.idx_s[t]] != t) return;  // a repeat no scan visits
   const f2 p = sl.pp_s[t];
   const float r = cfg->smoothing_radius, r2 = r * r;
@@ -1962,6 +1964,21 @@ __global__ __launch_bounds__(kBlock) void sph_runs_kernel(SphLayoutArgs a, const
   if (valid && next != e.x) a.run_end[e.x] = t + 1u;
   if (valid) a.run2[t] = make_uint2(0xFFFFFFFFu, 0u);  // no run for key t until the scan / write kernels
   const bool start = valid && e.x != prev;
+  // The bitmap of keys with a run (the fixup gathers run2 only for those: almost no empty cell's
+  // key has one).  Keys rise along the wave, so lanes sharing a 32-key word are adjacent: an
+  // OR-scan within each word's segment, one atomicOr per word and wave.
+  {
+    const uint32_t word = valid ? e.x >> 5 : 0xFFFFFFFFu;
+    uint32_t bits = start ? 1u << (e.x & 31u) : 0u;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint32_t ob = (uint32_t)__shfl_down((int)bits, d, 64);
+      const uint32_t ow = (uint32_t)__shfl_down((int)word, d, 64);
+      if (lane + d < 64u && ow == word) bits |= ob;
+    }
+    const uint32_t pw = (uint32_t)__shfl_up((int)word, 1, 64);
+    if (valid && bits && (lane == 0u || pw != word)) atomicOr(&a.keybits[word], bits);
+  }
   // Run lengths without a walk: a run starting in this wave ends at the wave's next run start
   // or, for the wave's last run, where the 64 slots after the wave first hold another key (one
   // coalesced load per lane; a run reaching past them is longer than kRunScan, so listed).
@@ -2129,7 +2146,8 @@ __global__ __launch_bounds__(kBlock) void sph_layout_fixup_kernel(SphLayoutArgs 
   if (a.cellrun[c].x == kCellPending) {
     int32_t cx, cy;
     grid_cell(a.g, c, cx, cy);
-    a.cellrun[c] = a.run2[cell_key(cx, cy, N)];
+    const uint32_t k = cell_key(cx, cy, N);
+    a.cellrun[c] = (a.keybits[k >> 5] >> (k & 31u)) & 1u ? a.run2[k] : make_uint2(0xFFFFFFFFu, 0u);
   }
 }
 
@@ -2445,7 +2463,7 @@ int sph_batch(bool density, uint32_t p, int forced, bool layout) {
 }
 
 static RunBounds run_bounds(const SphBuffers& b) {
-  return RunBounds{b.offsets, b.ends, b.lay.cellrun, b.lay.run2, b.lay.g};
+  return RunBounds{b.offsets, b.ends, b.lay.cellrun, b.lay.run2, b.lay.g, b.lay.keybits};
 }
 
 static hipError_t launch_sph_density(const SphBuffers& b, hipStream_t s) {
