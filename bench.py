@@ -1,13 +1,16 @@
 #!/usr/bin/env python3
 """bench.py — particle-updates/s of the per-particle step on MI355X (BASELINE.json metric).
 
-Workload (BASELINE.json configs[2]): 1e8 particles per GPU, 4 attractors
-moving on circles, drag, lifetime decay + Philox respawn, semi-implicit Euler, walls.  One
-"step" = one fused stream-kernel launch over every particle (in place, tiled SoA; 40 B per
-particle of algorithmic traffic per SURVEY §8(d), of which the kernel moves 32.03: x, y, vx, vy
-read+written and a u16 per group of 64 particles naming its earliest lifetime expiry).  Multi-GPU: one process per GPU, contiguous index shards with global particle ids, no
-data-path collective (weak scaling: 1e8 particles per rank).  Side lines: "sph", the
-reference's five-pass SPH frame at 2^22 particles (replicas); "allpairs", the all-pairs
+Workload (BASELINE.json configs[2]): 1e8 particles in all, 4 attractors moving
+on circles, drag, lifetime decay + Philox respawn, semi-implicit Euler, walls.  One "step" = one
+fused stream-kernel launch over every particle of the rank's shard (in place, tiled SoA).  The
+kernel moves 32.03 B per particle-step (x, y, vx, vy read+written and a u16 per group of 64
+particles naming its earliest lifetime expiry); SURVEY §8(d)'s 40 B counted an f32 lifetime that
+this representation never moves, so `roofline` divides the moved bytes.
+Multi-GPU: one process per GPU, the 1e8 particles split into contiguous index shards with
+global particle ids, no data-path collective: the metric's configuration at every N (strong
+scaling; `--particles P` instead runs P particles per GPU, weak scaling).  Side lines: "sph",
+the reference's five-pass SPH frame at 2^22 particles (replicas); "allpairs", the all-pairs
 N-body step with its RCCL all-gather, strong-scaled over the ranks.
 
     python bench.py [--gpus N --steps K --warmup W]
@@ -34,13 +37,13 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector peak at the 2400-MHz max clock
 FP32_PEAK_CLOCK_MHZ = 2400.0
 L2_PEAK_GBPS = 34500.0  # MI355X_MICROARCH.md §L2: aggregate over the 8 XCDs, ~34.5 TB/s
-# SURVEY.md §8(d) / BASELINE.md, C3: the algorithmic cost of a particle-step is 40 B (read and
-# write x, y, vx, vy and an f32 lifetime).  The kernel moves 32.03 of them (the lifetime is a u16
-# expiry read and written only in the group-steps where one is due, found from a u16 per group
-# of 64 particles:
-# DESIGN.md §3.2, §4): that figure is reported beside it as `moved_*`, and `traffic` is what
-# the PMC counters measured.
+# SURVEY.md §8(d) / BASELINE.md, C3 counted 40 B per particle-step (read and write x, y, vx, vy
+# and an f32 lifetime).  The kernel keeps the lifetime as a u16 expiry read and written only in the
+# group-steps where one is due, found from a u16 per group of 64 particles:
+# it moves 32.03 B, the figure `roofline.achieved` / `frac` use (rps_step_cost); the 40-B rate is
+# reported beside it as `algorithmic_equiv_gbps`, and `traffic` is what the PMC counters measured.
 ALGO_BYTES_PER_PARTICLE = 40.0
+GLOBAL_PARTICLES = 100_000_000  # BASELINE.json metric: 10^8 particles at 1/2/4/8 GPUs
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
@@ -49,7 +52,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=100)
-    ap.add_argument("--particles", type=int, default=100_000_000, help="particles per GPU")
+    ap.add_argument("--global-particles", type=int, default=GLOBAL_PARTICLES,
+                    help="particles over all ranks, split into contiguous shards (strong scaling; the metric's 1e8)")
+    ap.add_argument("--particles", type=int, default=0,
+                    help="particles per GPU instead (weak scaling: the global count grows with N); 0: strong")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget")
     ap.add_argument("--cpu-sample", type=int, default=1 << 22, help="CPU-baseline particles")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -170,8 +176,19 @@ def load_impl():
     return importlib.import_module(stub) if stub else importlib.import_module("rps_amd")
 
 
-def workload(rps, n_rank, world):
-    cfg = rps.default_particle_config(min(n_rank * world, 0xFFFFFFFF), gravity=0.0)
+def shard(args, d):
+    """(particles of this rank, its first global id, global particles).  Strong scaling (the
+    default): the global count split into contiguous index ranges, rank r owning
+    [r·G/W, (r+1)·G/W).  Weak (`--particles P`): P per rank, G = P·W."""
+    if args.particles:
+        return args.particles, d.rank * args.particles, args.particles * d.world
+    g = args.global_particles
+    lo, hi = g * d.rank // d.world, g * (d.rank + 1) // d.world
+    return hi - lo, lo, g
+
+
+def workload(rps, n_global):
+    cfg = rps.default_particle_config(min(n_global, 0xFFFFFFFF), gravity=0.0)
     ext = rps.headline_ext(stats=True)  # stats reduced every 100 steps (amortised)
     ext.shader_delay = 0  # every timed step is an active step
     return cfg, ext
@@ -187,13 +204,18 @@ def global_stats(d, st):
             "respawned_last": int(resp), "particles": int(parts), "ranks": d.world}
 
 
-def pmc_traffic(workload_name):
+def pmc_traffic(workload_name, n_rank):
+    """The dominant kernel's HBM bytes per launch from the committed PMC run of this workload
+    (profiles/pmc_traffic.json, tools/pmc_table.py), when that run processed the same number of
+    particles per launch as this rank; None otherwise (shards of another size)."""
     try:
         with open(PMC_FILE) as f:
-            d = json.load(f)
-        return d.get(workload_name, {}).get("hbm_bytes_per_launch")
+            rec = json.load(f).get("C3-1e8-4att-drag-respawn-euler", {})
     except (OSError, ValueError):
         return None
+    if not rec or rec.get("particles_per_launch", 100_000_000) != n_rank:
+        return None
+    return rec.get("hbm_bytes_per_launch")
 
 
 def pmc_sph():
@@ -213,7 +235,7 @@ def cpu_baseline(rps, args, cfg, ext):
 
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     n = args.cpu_sample
-    soa = orc.init_scatter(cfg, ext, args.seed, n, global_count=args.particles)
+    soa = orc.init_scatter(cfg, ext, args.seed, n, global_count=args.global_particles)
     orc.stream_step_omp(cfg, ext, soa, 0, threads=threads)  # warm (page-in, thread pool)
     t0 = time.perf_counter()
     steps = 0
@@ -547,11 +569,11 @@ def main():
     early = {}
     run_sides(rps, args, d, early, first)
 
-    n = args.particles
-    cfg, ext = workload(rps, n, d.world)
-    wl = "C3-1e8-4att-drag-respawn-euler"
+    n, id_offset, n_global = shard(args, d)
+    cfg, ext = workload(rps, n_global)
+    wl = f"C3-{n_global:.0e}-4att-drag-respawn-euler".replace("e+0", "e").replace("e+", "e")
     ctx = rps.Context(n, rps.MODE_STREAM, device=d.local if d.dist else 0,
-                      id_offset=d.rank * n, global_count=d.world * n)
+                      id_offset=id_offset, global_count=n_global)
     ctx.set_config(cfg, ext)
     if d.dist:  # under a launcher the stats steps all-reduce over the ranks inside librps (RCCL)
         ctx.comm_init(d.rank, d.world, d.broadcast_bytes(rps.comm_unique_id() if d.rank == 0 else b""))
@@ -569,7 +591,8 @@ def main():
     # The K steps between one pair of HIP events on the context stream (rps_time_steps): the
     # average launch is their span / K.  Launches run back to back (no event between them:
     # round 2 bracketed launches one by one, and each event pair left a ~12-us idle gap on the
-    # GPU); the span includes the stats steps that fall in the region.
+    # GPU); the span includes the stats steps that fall in the region (one
+    # two-kernel fold every 100th step, ~10 us).
     gpu_ms = ctx.time_steps(args.steps)
     ctx.sync()
     d.sync_device()
@@ -577,9 +600,10 @@ def main():
     d.barrier()
     elapsed = d.max(t1 - t0)
     kern_ms = d.max(gpu_ms / args.steps)
-    launches = args.steps
     moved_per_launch, _ = ctx.step_cost()  # bytes the kernel moves: 32.03 B per particle
-    algo_per_launch = ALGO_BYTES_PER_PARTICLE * n
+    moved_per_launch = d.max(moved_per_launch)  # the largest shard (ragged splits)
+    n_max = int(d.max(float(n)))
+    algo_per_launch = ALGO_BYTES_PER_PARTICLE * n_max
     if do_export and args.export_after:
         export = export_side(ctx, n, args.export_reps)
     if d.dist:
@@ -588,12 +612,13 @@ def main():
         stats, stats_ok = global_stats(d, ctx.stats()), True
     ctx.close()
 
-    updates = float(n) * d.world * args.steps
+    updates = float(n_global) * args.steps
     value = updates / elapsed
-    achieved = algo_per_launch / (kern_ms * 1e-3) / 1e9
-    moved_gbps = moved_per_launch / (kern_ms * 1e-3) / 1e9
+    achieved = moved_per_launch / (kern_ms * 1e-3) / 1e9  # the slowest rank's kernel, its bytes
+    algo_gbps = algo_per_launch / (kern_ms * 1e-3) / 1e9
     hbm_wall = moved_per_launch * args.steps / elapsed / 1e9  # per GPU, wall clock incl. gaps
-    traffic = pmc_traffic(wl)
+    traffic = pmc_traffic(wl, n_max)
+    strong = not args.particles
     line = {
         "metric": METRIC,
         "value": value,
@@ -603,25 +628,30 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed * 1e3 / args.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (seeded device scatter of src/main.rs:182-216; Philox respawn)",
-        "config": {"workload": wl, "particles_per_gpu": n, "global_particles": n * d.world,
+        "config": {"workload": wl, "global_particles": n_global, "particles_per_gpu": n_max,
                    "attractors": 4, "drag": 0.1, "lifetime_s": [1.0, 5.0], "integrator": "euler",
-                   "bytes_per_particle_step": moved_per_launch / n, "parallelism": f"index-shard x{d.world}"},
+                   "bytes_per_particle_step": moved_per_launch / n_max,
+                   "parallelism": f"index-shard x{d.world} ({'strong: the global count split' if strong else 'weak: per-GPU count fixed'})"},
         "hbm_gbps_per_gpu": hbm_wall,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS,
                      "traffic": traffic, "kernel": "stream_step_kernel<euler,lifetime>",
-                     "avg_kernel_ms": kern_ms, "launches": launches,
-                     "timing": "one HIP event pair on the context stream around the K timed launches",
-                     "algorithmic_bytes_per_launch": algo_per_launch,
-                     "moved_bytes_per_launch": moved_per_launch, "moved_gbps": moved_gbps,
-                     "moved_frac": moved_gbps / HBM_PEAK_GBPS,
-                     "note": "achieved/frac use SURVEY 8(d)'s 40 algorithmic bytes per particle-step; the "
-                             "kernel moves 32.03 of them (u16 expiry behind a per-group index), so frac can "
-                             "exceed 1; moved_frac is the HBM utilisation"},
+                     "avg_kernel_ms": kern_ms, "launches": args.steps,
+                     "timing": "one HIP event pair on the context stream around the K timed launches "
+                               "(includes the stats fold of any 100th step in the region); max over ranks",
+                     "bytes_per_launch": moved_per_launch,
+                     "bytes_basis": "bytes the kernel moves (rps_step_cost: 32.03 B per particle; PMC agrees "
+                                    "within 0.3 %, profiles/pmc_traffic.json)",
+                     "algorithmic_bytes_per_launch_survey": algo_per_launch,
+                     "algorithmic_equiv_gbps": algo_gbps,
+                     "note": "SURVEY 8(d)'s 40 B per particle-step counts an f32 lifetime read and written every "
+                             "step; the kernel keeps a u16 expiry behind a per-group index and moves 32.03 B, "
+                             "so the utilisation is the moved bytes' rate (DESIGN.md §5.1); "
+                             "algorithmic_equiv_gbps is the 40-B rate, an equivalence, not traffic"},
         "stats": stats,
     }
     if export is not None:

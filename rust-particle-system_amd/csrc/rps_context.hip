@@ -56,6 +56,8 @@ struct rps_ctx {
   SphLayoutArgs lay{};     // spatial record layout (P == N, RPS_SPH_LAYOUT != 0): arrays
   uint32_t cell_cap = 0;   // their cell capacity (0: no layout)
   bool layout_last = false;  // the last active frame used the layout (slot records in storage order)
+  uint32_t* longq_cnt = nullptr;  // the long-scan queue's two counters (SphSlots::longq; P != N)
+  uint32_t longq_par = 0;         // which of them the next active frame appends to
   bool last_frame_active = false;  // the most recent frame ran passes 4-5 (rps_sph_frame_cost)
   unsigned long long* d_count = nullptr;  // rps_sph_frame_cost's per-workgroup counts (SPH)
   // Slot-resident state (layout frames): after a layout frame st holds the
@@ -490,6 +492,11 @@ int sph_frame_begin(rps_ctx* ctx, bool layout) {
 int step_sph_sim(rps_ctx* ctx, bool layout, const SphGrid& g) {
   ctx->layout_last = layout;
   if (layout) ctx->lay.g = g;
+  if (ctx->sl.longq) {  // this frame's queue counter, and the one its density pass zeroes
+    ctx->sl.longq_n = ctx->longq_cnt + ctx->longq_par;
+    ctx->sl.longq_next = ctx->longq_cnt + (ctx->longq_par ^ 1u);
+    ctx->longq_par ^= 1u;
+  }
   SphBuffers b = sph_buffers(ctx);
   if (layout)
     RPS_HIP(ctx, launch_sph_layout_pre(b, ctx->stream));
@@ -626,6 +633,12 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     slots.push_back({(void**)&ctx->ends, align_up(n * sizeof(uint32_t), 256)});
     slots.push_back({(void**)&ctx->sl.nbr_mask, align_up(2 * P * sizeof(uint64_t), 256)});
     if (P != n) slots.push_back({(void**)&ctx->sl.owner, align_up(n * sizeof(uint32_t), 256)});
+    // Long scans one per wave (rps_kernels.hip, kLongScan): P != N, where the reference's pad
+    // hazard grows long duplicate runs.  RPS_SPH_LONGQ=0 keeps them in their lanes (A/B).
+    if (P != n && env_int("RPS_SPH_LONGQ", 1) != 0) {
+      slots.push_back({(void**)&ctx->sl.longq, align_up(P * sizeof(uint32_t), 256)});
+      slots.push_back({(void**)&ctx->longq_cnt, 256});
+    }
     slots.push_back({(void**)&ctx->lookup, align_up((size_t)ctx->P * sizeof(uint2), 256)});
     slots.push_back({(void**)&ctx->offsets, align_up(n * sizeof(uint32_t), 256)});
     slots.push_back({(void**)&ctx->dens, align_up(n * sizeof(f2), 256)});

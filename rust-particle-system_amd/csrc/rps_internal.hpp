@@ -112,6 +112,13 @@ struct SphSlots {
   // slots repeat particles; a repeat computes exactly its owner's values, so the
   // sim runs on owner slots only, and slots >= N (never a neighbour entry) skip the density too.
   uint32_t* owner;
+  // P != N only (else nullptr): the slots whose nine runs hold more than kLongScan entries,
+  // appended by the density pass and computed one per wave by the long-scan kernels
+  // (rps_kernels.hip).  longq_n counts this active frame's entries; longq_next is the other of
+  // two counters, which the density pass zeroes for the next active frame.
+  uint32_t* longq;
+  uint32_t* longq_n;
+  uint32_t* longq_next;
 };
 // Cell range of the spatial record layout (rps_kernels.hip): cells [cx_lo, cx_lo + w) x
 // [cy_lo, cy_lo + h), enumerated in 8 x 8 tiles, tw tiles per row; cells = tiles x 64.

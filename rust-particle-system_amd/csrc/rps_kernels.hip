@@ -1556,6 +1556,41 @@ struct RunCursor {
   }
 };
 
+// Long scans (P != N).  The reference's pad hazard keeps the top P - N entries of
+// each frame's sort as stale duplicates that sort back in, so at N = 50 000 the runs of the keys
+// near N grow to 150+ entries and a particle near such a cell scans 200+ entries; its lane's
+// chain of dependent batches was the density and sim kernels' critical path (5.7x the 65 536
+// kernel time for 1.5x the work).  Slots whose nine runs hold more than kLongScan entries (those
+// the sim scans without a mask anyway) are appended to a queue by the density kernel and
+// computed one slot per WAVE by sph_density_long_kernel and sph_sim_long_kernel: 64 lanes
+// load and evaluate 64 consecutive entries at once, and the sums are taken entry by entry in
+// the reference's order from the lanes' terms (v_readlane), so every particle's sums are the
+// same additions in the same order as in its own lane.
+// A particle whose own position is not finite stays in its lane: its sums are NaN from its
+// first entry on, and both scans stop after one batch.
+constexpr uint32_t kLongScan = 128u;
+constexpr uint32_t kLongSub = 4;  // entries per lane in flight in the long-scan kernels (256 per wave)
+__device__ __forceinline__ bool long_scan(uint32_t total, f2 p) {
+  return total > kLongScan && fabsf(p[0]) < INFINITY && fabsf(p[1]) < INFINITY;
+}
+
+__device__ __forceinline__ float readlane_f(float v, uint32_t lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)lane));
+}
+
+// Appends v for every lane with `want` to q (one atomic per wave).
+__device__ __forceinline__ void wave_append(bool want, uint32_t* count, uint32_t* q, uint32_t v) {
+  const uint64_t m = __builtin_amdgcn_ballot_w64(want);
+  if (!m) return;
+  const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+  const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  uint32_t base = 0u;
+  if (lane == leader) base = atomicAdd(count, (uint32_t)__builtin_popcountll(m));
+  base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)leader);
+  const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  if (want) q[base + below] = v;
+}
+
 // Work mapping of the density and sim passes: thread t takes lookup slot t of all P.  Lanes
 // of a wave then hold the particles of a few cells and read the same runs together.  Every
 // particle's fresh entry is in exactly one slot; pad slots repeat some
@@ -1572,6 +1607,35 @@ struct RunCursor {
 // on both sides: the sim's (q - p)^2 sums equal the density's (p - q)^2 sums bit for bit.
 // A particle with more than 128 entries in its nine runs scans and tests them as before.
 //
+// One entry's density_kernel / near_density_kernel terms at squared distance sq (wgsl:176-189,
+// :246-250), for an entry within the radius.  Correctly rounded sqrt without the input scaling
+// unless a lane of the wave needs it (0 < sq < 2^-96: two particles closer than ~1e-14, only
+// ever near the origin): the same bits as sqrtf (tools/sqrt_check.hip, every input), 2^22
+// frame 1.2461 -> 1.2358 ms (same box).
+__device__ __forceinline__ f2 density_terms(float sq, float r, float dn, float ndn) {
+  const float dist = sqrt_rn_wave(sq);
+  float k1 = 0.0f, k2 = 0.0f;
+  if (!(dist >= r)) {
+    const float v = r - dist;
+    k1 = (dn * v) * v;
+    k2 = ((ndn * v) * v) * v;
+  }
+  return f2{k1, k2};
+}
+
+// The density pass's per-slot outputs: the neighbour mask, and the neighbour halves of
+// pressure_term / near_pressure_term (wgsl:323-327), which depend on this particle alone:
+// evaluated once here (same ops, same bits) instead of per visiting neighbour in the sim pass.
+__device__ __forceinline__ void density_store(const rps_config* __restrict__ cfg, const SphSlots& sl, uint32_t t,
+                                              uint32_t p_slots, f2 p, float d, float nd, uint64_t m0, uint64_t m1) {
+  sl.nbr_mask[t] = m0;
+  sl.nbr_mask[p_slots + t] = m1;
+  const float P = (d - cfg->target_density) * cfg->pressure_multiplier;  // wgsl:191-199
+  const float Pn = nd * cfg->near_density_multiplier;
+  sl.rec_pd[t] = f4{p[0], p[1], P / (d * d), Pn / (d * nd)};
+  sl.dens_s[t] = f2{d, nd};
+}
+
 // calculate_density, compute_shader.wgsl:207-254: entries summed in run order, kScanBatch
 // predicted positions in flight per lane across run boundaries.
 template <int kScanBatch, bool LAYOUT>
@@ -1595,9 +1659,20 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
   // §3.4).  With the particle's own position finite, the entry that made them NaN is another
   // particle's NaN (or infinite) position, already in the mask, and the sim's pressure term for
   // it is NaN in both components: the particle's state ends NaN whatever follows, so the scan
-  // stops there (the rest of the mask unset).  An own non-finite position scans everything.
+  // stops there (the rest of the mask unset).  An own non-finite position makes both sums NaN at
+  // the first entry, its own included, so its mask is what the sim's self-skipping scan needs in
+  // full; but with more than 128 entries the sim scans the runs and ignores the mask, so such a
+  // particle stops too (at N = 50 000 the NaN particles pile into the key-0 run, which each of
+  // them scanned whole: 2 180 entries by frame 70, the kernel's critical path).
   const bool own_finite = fabsf(p[0]) < INFINITY && fabsf(p[1]) < INFINITY;
-  for (uint32_t f = 0; f < total && !(own_finite && d != d && nd != nd); f += kScanBatch) {
+  if (sl.longq) {  // long scans go to sph_density_long_kernel (see there)
+    if (t == 0u) *sl.longq_next = 0u;  // the next active frame's count (its last use has ended)
+    const bool defer = long_scan(total, p);
+    wave_append(defer, sl.longq_n, sl.longq, t);
+    if (defer) return;
+  }
+  const bool may_stop = own_finite || total > 128u;
+  for (uint32_t f = 0; f < total && !(may_stop && d != d && nd != nd); f += kScanBatch) {
     f2 q[kScanBatch];
 #pragma unroll
     for (int u = 0; u < kScanBatch; ++u) q[u] = sl.pp_s[rc.slot(min(f + u, total - 1u))];
@@ -1612,32 +1687,54 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
             if (b < 64u) m0 |= 1ull << b;
             else m1 |= 1ull << (b - 64u);
           }
-          // Correctly rounded sqrt without the input scaling unless a lane of the wave needs it
-          // (0 < sq < 2^-96: two particles closer than ~1e-14, only ever near the origin):
-          // the same bits as sqrtf (tools/sqrt_check.hip, every input), 2^22 frame
-          // 1.2461 -> 1.2358 ms (same box).
-          const float dist = sqrt_rn_wave(sq);
-          float k1 = 0.0f, k2 = 0.0f;
-          if (!(dist >= r)) {
-            const float v = r - dist;
-            k1 = (dn * v) * v;
-            k2 = ((ndn * v) * v) * v;
-          }
-          d = d + k1;
-          nd = nd + k2;
+          const f2 k = density_terms(sq, r, dn, ndn);
+          d = d + k[0];
+          nd = nd + k[1];
         }
       }
     }
   }
-  sl.nbr_mask[t] = m0;
-  sl.nbr_mask[p_slots + t] = m1;
-  // The neighbour halves of pressure_term / near_pressure_term (wgsl:323-327) depend on this
-  // particle alone: evaluated once here (same ops, same bits) instead of per visiting
-  // neighbour in the sim pass.
-  const float P = (d - cfg->target_density) * cfg->pressure_multiplier;  // wgsl:191-199
-  const float Pn = nd * cfg->near_density_multiplier;
-  sl.rec_pd[t] = f4{p[0], p[1], P / (d * d), Pn / (d * nd)};
-  sl.dens_s[t] = f2{d, nd};
+  density_store(cfg, sl, t, p_slots, p, d, nd, m0, m1);
+}
+
+// A long scan of the density pass (kLongScan): one queued slot per wave, 64 entries per step.
+template <bool LAYOUT>
+__global__ __launch_bounds__(kBlock) void sph_density_long_kernel(const rps_config* __restrict__ cfg,
+                                                                  RunBounds rb, SphSlots sl, uint32_t p_slots) {
+  const uint32_t count = *sl.longq_n;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t nw = gridDim.x * (kBlock / 64u);
+  const uint32_t N = cfg->particle_count;
+  const float r = cfg->smoothing_radius, r2 = r * r;
+  const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
+  __shared__ RunTable runs;
+  for (uint32_t k = blockIdx.x * (kBlock / 64u) + (threadIdx.x >> 6); k < count; k += nw) {
+    const uint32_t t = sl.longq[k];
+    const f2 p = sl.pp_s[t];
+    // Every lane builds the slot's table in its own column: lane l then walks entries l, l + 64, ...
+    const uint32_t total = nine_runs<LAYOUT>(rb, p[0], p[1], cfg->screen_bounds[1], cfg->screen_bounds[3], r, N, runs);
+    RunCursor rc(runs);
+    float d = 0.0f, nd = 0.0f;
+    for (uint32_t f0 = 0; f0 < total; f0 += 64u * kLongSub) {
+      f2 q[kLongSub];
+#pragma unroll
+      for (uint32_t u = 0; u < kLongSub; ++u) q[u] = sl.pp_s[rc.slot_skip(min(f0 + 64u * u + lane, total - 1u))];
+#pragma unroll
+      for (uint32_t u = 0; u < kLongSub; ++u) {
+        const uint32_t f = f0 + 64u * u + lane;
+        const float dx = p[0] - q[u][0], dy = p[1] - q[u][1];
+        const float sq = dx * dx + dy * dy;
+        const f2 kk = density_terms(sq, r, dn, ndn);
+        for (uint64_t m = __builtin_amdgcn_ballot_w64(f < total && !(sq > r2)); m; m &= m - 1u) {
+          const uint32_t b = (uint32_t)__builtin_ctzll(m);  // entries in increasing f: the lane's order
+          d = d + readlane_f(kk[0], b);
+          nd = nd + readlane_f(kk[1], b);
+        }
+      }
+      if (d != d && nd != nd) break;  // NaN whatever follows (more than 128 entries: no mask)
+    }
+    if (lane == 0u) density_store(cfg, sl, t, p_slots, p, d, nd, 0ull, 0ull);
+  }
 }
 
 // Drivers of the sim pass's two scans: body(q) for every entry within the radius that is
@@ -1703,93 +1800,64 @@ __device__ __forceinline__ void scan_runs(const SphSlots& sl, const RunTable& ru
   }
 }
 
-// simulation_step, compute_shader.wgsl:435-453: pressure (:256-334) and viscosity
-// (:336-384) against the start-of-pass velocity snapshot (rec_pv.zw), Euler (:392-395) and
-// walls (:69-99).  The new packed state of particle i is written in place, st[i]: after the
-// predict pass nothing reads st in this frame (the scans read the slot records), so one state
-// buffer does; a second one (ping-pong) only added 64 MB at 2^22 to the frame's working set,
-// which is what decides whether the scattered 16-B writes merge in the Infinity Cache or go
-// to HBM as partial-line writes.
-template <int kScanBatch, bool kPads, bool LAYOUT>
-__global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __restrict__ cfg,
-                                                         RunBounds rb, SphSlots sl, f4* __restrict__ st,
-                                                         uint2* __restrict__ bin_next, uint32_t p_slots) {
-  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-  if (t >= p_slots) return;
+// One entry's pressure_force terms (wgsl:279-334) for an entry within the radius: the
+// pressure and near-pressure contributions {x, y, near x, near y}, each the product the
+// reference adds (the sums take them in that order).
+__device__ __forceinline__ f4 pressure_terms(const f4& q, f2 p, float P_rho2, float Pn_rho2, float r, float dn,
+                                             float ndn) {
+  const float dx = q[0] - p[0], dy = q[1] - p[1];
+  const float dist = sqrt_rn_wave(dx * dx + dy * dy);
+  float dirx, diry;
+  if (dist > 0.0001f) {
+    dirx = dx / dist;
+    diry = dy / dist;
+  } else {
+    dirx = 0.0f;
+    diry = 1.0f;
+  }
+  const float pt = P_rho2 + q[2];    // + Pj / (rj * rj)
+  const float npt = Pn_rho2 + q[3];  // + Pnj / (rj * rnj)
+  float dk = 0.0f, ndk = 0.0f;
+  if (!(dist >= r)) {
+    const float v = r - dist;
+    dk = (-2.0f * dn) * v;
+    ndk = ((-3.0f * ndn) * v) * v;
+  }
+  return f4{(dirx * pt) * dk, (diry * pt) * dk, (dirx * npt) * ndk, (diry * npt) * ndk};
+}
+
+// viscosity_kernel of an entry within the radius (wgsl:336-384): the weight of (v_j - v_i).
+__device__ __forceinline__ float viscosity_weight(const f4& q, f2 p, float r, float vn) {
+  const float dx = p[0] - q[0], dy = p[1] - q[1];
+  const float dist = sqrt_rn_wave(dx * dx + dy * dy);
+  float k = 0.0f;
+  if (!(dist >= r)) {
+    const float v = r * r - dist * dist;
+    k = ((vn * v) * v) * v;
+  }
+  return k;
+}
+
+// The sim pass's loop invariants of slot t (its particle i).
+struct SimOwn {
+  f2 p;
+  float P_rho2, Pn_rho2;  // loop-invariant halves of pressure_term and near_pressure_term (wgsl:323-327)
+  uint32_t i;
+};
+__device__ __forceinline__ SimOwn sim_own(const rps_config* __restrict__ cfg, const SphSlots& sl, uint32_t t) {
   const f4 own = sl.rec_pd[t];  // own predicted position (xy) and P / rho^2 (z)
   const f2 own_d = sl.dens_s[t];
-  const uint32_t i = sl.idx_s[t];
-  if (kPads && sl.owner[i] != t) return;  // a repeat: its owner slot computes the same state
-  const uint32_t self = kPads ? i : t;
-  const float dt = cfg->fixed_delta_time;
-  const float r = cfg->smoothing_radius, r2 = r * r;
-  const uint32_t N = cfg->particle_count;
-  const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
-  const float vn = cfg->viscocity_kernel_norm;
-  const f2 p = f2{own[0], own[1]};
   const float rho = own_d[0];
   const float Pn = own_d[1] * cfg->near_density_multiplier;
-  const float P_rho2 = own[2];             // loop-invariant halves of pressure_term and
-  const float Pn_rho2 = Pn / (rho * rho);  // near_pressure_term (wgsl:323-327)
-  __shared__ RunTable runs;
-  const uint32_t total = nine_runs<LAYOUT>(rb, p[0], p[1], cfg->screen_bounds[1],
-                                   cfg->screen_bounds[3], r, N, runs);
-  const bool masked = total <= 128u;
-  const uint64_t m0 = masked ? sl.nbr_mask[t] : 0u, m1 = masked ? sl.nbr_mask[p_slots + t] : 0u;
-  float fx = 0.0f, fy = 0.0f;
-  const auto load_pd = [&](uint32_t j) { return sl.rec_pd[j]; };
-  const auto pressure = [&](const f4& q) {
-    const float dx = q[0] - p[0], dy = q[1] - p[1];
-    const float dist = sqrt_rn_wave(dx * dx + dy * dy);
-    float dirx, diry;
-    if (dist > 0.0001f) {
-      dirx = dx / dist;
-      diry = dy / dist;
-    } else {
-      dirx = 0.0f;
-      diry = 1.0f;
-    }
-    const float pt = P_rho2 + q[2];    // + Pj / (rj * rj)
-    const float npt = Pn_rho2 + q[3];  // + Pnj / (rj * rnj)
-    float dk = 0.0f, ndk = 0.0f;
-    if (!(dist >= r)) {
-      const float v = r - dist;
-      dk = (-2.0f * dn) * v;
-      ndk = ((-3.0f * ndn) * v) * v;
-    }
-    fx = fx + (dirx * pt) * dk;
-    fy = fy + (diry * pt) * dk;
-    fx = fx + (dirx * npt) * ndk;
-    fy = fy + (diry * npt) * ndk;
-  };
-  // A force sum that is NaN in both components stays NaN whatever is added (payloads aside,
-  // DESIGN.md §3.4): the scan stops there.  Only a particle whose state ends NaN gets there.
-  const auto pressure_nan = [&] { return fx != fx && fy != fy; };
-  if (masked)
-    scan_masked<kScanBatch, kPads>(sl, runs, m0, m1, self, load_pd, pressure, pressure_nan);
-  else
-    scan_runs<kScanBatch, kPads>(sl, runs, 0u, total, p, r2, self, load_pd, pressure, pressure_nan);
-  const f4 own_pv = sl.rec_pv[t];
-  float qx = own_pv[2] + fx * dt;  // post-gravity velocity (the pre pass, wgsl:397-400)
-  float qy = own_pv[3] + fy * dt;
-  float wx = 0.0f, wy = 0.0f;
-  const auto load_pv = [&](uint32_t j) { return sl.rec_pv[j]; };
-  const auto viscosity = [&](const f4& q) {
-    const float dx = p[0] - q[0], dy = p[1] - q[1];
-    const float dist = sqrt_rn_wave(dx * dx + dy * dy);
-    float k = 0.0f;
-    if (!(dist >= r)) {
-      const float v = r * r - dist * dist;
-      k = ((vn * v) * v) * v;
-    }
-    wx = wx + (q[2] - qx) * k;
-    wy = wy + (q[3] - qy) * k;
-  };
-  const auto viscosity_nan = [&] { return wx != wx && wy != wy; };
-  if (masked)
-    scan_masked<kScanBatch, kPads>(sl, runs, m0, m1, self, load_pv, viscosity, viscosity_nan);
-  else
-    scan_runs<kScanBatch, kPads>(sl, runs, 0u, total, p, r2, self, load_pv, viscosity, viscosity_nan);
+  return SimOwn{f2{own[0], own[1]}, own[2], Pn / (rho * rho), sl.idx_s[t]};
+}
+
+// Viscosity applied, Euler (wgsl:392-395), walls (:69-99) and the store of slot t's new state.
+template <bool LAYOUT>
+__device__ __forceinline__ void sim_finish(const rps_config* __restrict__ cfg, const SphSlots& sl, f4* __restrict__ st,
+                                           uint2* __restrict__ bin_next, uint32_t t, uint32_t i, float qx, float qy,
+                                           float wx, float wy) {
+  const float dt = cfg->fixed_delta_time;
   qx = qx + (wx * cfg->viscocity_strength) * dt;
   qy = qy + (wy * cfg->viscocity_strength) * dt;
   const f2 c = sl.cur_s[t];
@@ -1802,11 +1870,160 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
     // scatter), and the next frame's bin entry of particle i (bin_key's ops on the same
     // position and config), which the next head launch reads in place of the positions.
     st[t] = f4{ox, oy, qx, qy};
+    const float r = cfg->smoothing_radius;
     const int32_t cx = f32_to_i32((ox + cfg->screen_bounds[1]) / r);
     const int32_t cy = f32_to_i32((oy + cfg->screen_bounds[3]) / r);
-    bin_next[i] = make_uint2(cell_key(cx, cy, N), t);
+    bin_next[i] = make_uint2(cell_key(cx, cy, cfg->particle_count), t);
   } else {
     st[i] = f4{ox, oy, qx, qy};
+  }
+}
+
+// simulation_step, compute_shader.wgsl:435-453: pressure (:256-334) and viscosity
+// (:336-384) against the start-of-pass velocity snapshot (rec_pv.zw), Euler (:392-395) and
+// walls (:69-99).  The new packed state of particle i is written in place, st[i]: after the
+// predict pass nothing reads st in this frame (the scans read the slot records), so one state
+// buffer does; a second one (ping-pong) only added 64 MB at 2^22 to the frame's working set,
+// which is what decides whether the scattered 16-B writes merge in the Infinity Cache or go
+// to HBM as partial-line writes.  Slots the density pass queued (long scans)
+// are left to sph_sim_long_kernel.
+template <int kScanBatch, bool kPads, bool LAYOUT>
+__global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __restrict__ cfg,
+                                                         RunBounds rb, SphSlots sl, f4* __restrict__ st,
+                                                         uint2* __restrict__ bin_next, uint32_t p_slots) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= p_slots) return;
+  const SimOwn o = sim_own(cfg, sl, t);
+  if (kPads && sl.owner[o.i] != t) return;  // a repeat: its owner slot computes the same state
+  const uint32_t self = kPads ? o.i : t;
+  const float dt = cfg->fixed_delta_time;
+  const float r = cfg->smoothing_radius, r2 = r * r;
+  const uint32_t N = cfg->particle_count;
+  const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
+  const float vn = cfg->viscocity_kernel_norm;
+  const f2 p = o.p;
+  __shared__ RunTable runs;
+  const uint32_t total = nine_runs<LAYOUT>(rb, p[0], p[1], cfg->screen_bounds[1],
+                                   cfg->screen_bounds[3], r, N, runs);
+  const bool masked = total <= 128u;
+  if (sl.longq && long_scan(total, p)) return;  // queued by the density pass
+  const uint64_t m0 = masked ? sl.nbr_mask[t] : 0u, m1 = masked ? sl.nbr_mask[p_slots + t] : 0u;
+  float fx = 0.0f, fy = 0.0f;
+  const auto load_pd = [&](uint32_t j) { return sl.rec_pd[j]; };
+  const auto pressure = [&](const f4& q) {
+    const f4 w = pressure_terms(q, p, o.P_rho2, o.Pn_rho2, r, dn, ndn);
+    fx = fx + w[0];
+    fy = fy + w[1];
+    fx = fx + w[2];
+    fy = fy + w[3];
+  };
+  // A force sum that is NaN in both components stays NaN whatever is added (payloads aside,
+  // DESIGN.md §3.4): the scan stops there.  Only a particle whose state ends NaN gets there.
+  const auto pressure_nan = [&] { return fx != fx && fy != fy; };
+  if (masked)
+    scan_masked<kScanBatch, kPads>(sl, runs, m0, m1, self, load_pd, pressure, pressure_nan);
+  else
+    scan_runs<kScanBatch, kPads>(sl, runs, 0u, total, p, r2, self, load_pd, pressure, pressure_nan);
+  const f4 own_pv = sl.rec_pv[t];
+  const float qx = own_pv[2] + fx * dt;  // post-gravity velocity (the pre pass, wgsl:397-400)
+  const float qy = own_pv[3] + fy * dt;
+  float wx = 0.0f, wy = 0.0f;
+  const auto load_pv = [&](uint32_t j) { return sl.rec_pv[j]; };
+  const auto viscosity = [&](const f4& q) {
+    const float k = viscosity_weight(q, p, r, vn);
+    wx = wx + (q[2] - qx) * k;
+    wy = wy + (q[3] - qy) * k;
+  };
+  const auto viscosity_nan = [&] { return wx != wx && wy != wy; };
+  if (masked)
+    scan_masked<kScanBatch, kPads>(sl, runs, m0, m1, self, load_pv, viscosity, viscosity_nan);
+  else
+    scan_runs<kScanBatch, kPads>(sl, runs, 0u, total, p, r2, self, load_pv, viscosity, viscosity_nan);
+  sim_finish<LAYOUT>(cfg, sl, st, bin_next, t, o.i, qx, qy, wx, wy);
+}
+
+// The sim pass of the density pass's queued slots (kLongScan), one per wave: lane l evaluates
+// flat entries l, l + 64, ... of both scans; the sums add the lanes' terms entry by entry.
+template <bool kPads, bool LAYOUT>
+__global__ __launch_bounds__(kBlock) void sph_sim_long_kernel(const rps_config* __restrict__ cfg,
+                                                              RunBounds rb, SphSlots sl, f4* __restrict__ st,
+                                                              uint2* __restrict__ bin_next) {
+  const uint32_t count = *sl.longq_n;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t nw = gridDim.x * (kBlock / 64u);
+  const float dt = cfg->fixed_delta_time;
+  const float r = cfg->smoothing_radius, r2 = r * r;
+  const uint32_t N = cfg->particle_count;
+  const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
+  const float vn = cfg->viscocity_kernel_norm;
+  __shared__ RunTable runs;
+  for (uint32_t k = blockIdx.x * (kBlock / 64u) + (threadIdx.x >> 6); k < count; k += nw) {
+    const uint32_t t = sl.longq[k];
+    const SimOwn o = sim_own(cfg, sl, t);
+    if (kPads && sl.owner[o.i] != t) continue;  // a repeat (wave-uniform)
+    const uint32_t self = kPads ? o.i : t;
+    const f2 p = o.p;
+    const uint32_t total = nine_runs<LAYOUT>(rb, p[0], p[1], cfg->screen_bounds[1], cfg->screen_bounds[3], r, N, runs);
+    // The entries of both scans: within the radius and not the particle itself (scan_runs);
+    // kLongSub per lane in flight, entry f = f0 + 64 u + lane.
+    const auto gather = [&](RunCursor& rc, uint32_t f0, const f4* rec, f4 (&q)[kLongSub], bool (&in)[kLongSub]) {
+      uint32_t j[kLongSub], qi[kLongSub];
+#pragma unroll
+      for (uint32_t u = 0; u < kLongSub; ++u) j[u] = rc.slot_skip(min(f0 + 64u * u + lane, total - 1u));
+#pragma unroll
+      for (uint32_t u = 0; u < kLongSub; ++u) {
+        q[u] = rec[j[u]];
+        qi[u] = kPads ? sl.idx_s[j[u]] : j[u];
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kLongSub; ++u) {
+        const float dx = q[u][0] - p[0], dy = q[u][1] - p[1];
+        in[u] = f0 + 64u * u + lane < total && qi[u] != self && !(dx * dx + dy * dy > r2);
+      }
+    };
+    float fx = 0.0f, fy = 0.0f;
+    {
+      RunCursor rc(runs);
+      for (uint32_t f0 = 0; f0 < total && !(fx != fx && fy != fy); f0 += 64u * kLongSub) {
+        f4 q[kLongSub];
+        bool in[kLongSub];
+        gather(rc, f0, sl.rec_pd, q, in);
+#pragma unroll
+        for (uint32_t u = 0; u < kLongSub; ++u) {
+          const f4 w = pressure_terms(q[u], p, o.P_rho2, o.Pn_rho2, r, dn, ndn);
+          for (uint64_t m = __builtin_amdgcn_ballot_w64(in[u]); m; m &= m - 1u) {
+            const uint32_t b = (uint32_t)__builtin_ctzll(m);
+            fx = fx + readlane_f(w[0], b);
+            fy = fy + readlane_f(w[1], b);
+            fx = fx + readlane_f(w[2], b);
+            fy = fy + readlane_f(w[3], b);
+          }
+        }
+      }
+    }
+    const f4 own_pv = sl.rec_pv[t];
+    const float qx = own_pv[2] + fx * dt;
+    const float qy = own_pv[3] + fy * dt;
+    float wx = 0.0f, wy = 0.0f;
+    {
+      RunCursor rc(runs);
+      for (uint32_t f0 = 0; f0 < total && !(wx != wx && wy != wy); f0 += 64u * kLongSub) {
+        f4 q[kLongSub];
+        bool in[kLongSub];
+        gather(rc, f0, sl.rec_pv, q, in);
+#pragma unroll
+        for (uint32_t u = 0; u < kLongSub; ++u) {
+          const float kw = viscosity_weight(q[u], p, r, vn);
+          const float tx = (q[u][2] - qx) * kw, ty = (q[u][3] - qy) * kw;
+          for (uint64_t m = __builtin_amdgcn_ballot_w64(in[u]); m; m &= m - 1u) {
+            const uint32_t b = (uint32_t)__builtin_ctzll(m);
+            wx = wx + readlane_f(tx, b);
+            wy = wy + readlane_f(ty, b);
+          }
+        }
+      }
+    }
+    if (lane == 0u) sim_finish<LAYOUT>(cfg, sl, st, bin_next, t, o.i, qx, qy, wx, wy);
   }
 }
 
@@ -2466,6 +2683,9 @@ static RunBounds run_bounds(const SphBuffers& b) {
   return RunBounds{b.offsets, b.ends, b.lay.cellrun, b.lay.run2, b.lay.g, b.lay.keybits};
 }
 
+// Workgroups of the long-scan kernels (4 waves each, a wave per queued slot in turn).
+static uint32_t long_blocks(uint32_t p) { return std::min<uint32_t>(blocks_for(p), 512u); }
+
 static hipError_t launch_sph_density(const SphBuffers& b, hipStream_t s) {
   const RunBounds rb = run_bounds(b);
 #define RPS_DENSITY(B)                                                                            \
@@ -2481,6 +2701,14 @@ static hipError_t launch_sph_density(const SphBuffers& b, hipStream_t s) {
     default: RPS_DENSITY(8); break;
   }
 #undef RPS_DENSITY
+  if (b.sl.longq) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (b.layout)
+      hipLaunchKernelGGL((sph_density_long_kernel<true>), dim3(long_blocks(b.p)), dim3(kBlock), 0, s, b.cfg, rb, b.sl, b.p);
+    else
+      hipLaunchKernelGGL((sph_density_long_kernel<false>), dim3(long_blocks(b.p)), dim3(kBlock), 0, s, b.cfg, rb, b.sl, b.p);
+  }
   return hipGetLastError();
 }
 
@@ -2557,6 +2785,17 @@ hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s) {
     default: RPS_SIM(8); break;
   }
 #undef RPS_SIM
+  if (b.sl.longq) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const dim3 g(long_blocks(b.p));
+    if (b.layout)
+      hipLaunchKernelGGL((sph_sim_long_kernel<false, true>), g, dim3(kBlock), 0, s, b.cfg, rb, b.sl, b.st, b.bin_next);
+    else if (b.p == b.n)
+      hipLaunchKernelGGL((sph_sim_long_kernel<false, false>), g, dim3(kBlock), 0, s, b.cfg, rb, b.sl, b.st, b.bin_next);
+    else
+      hipLaunchKernelGGL((sph_sim_long_kernel<true, false>), g, dim3(kBlock), 0, s, b.cfg, rb, b.sl, b.st, b.bin_next);
+  }
   return hipGetLastError();
 }
 

@@ -38,7 +38,7 @@ def _shard(rank, n):
 
 class Context:
     def __init__(self, n, mode=MODE_STREAM, device=0, id_offset=0, global_count=None):
-        self.n, self.mode = n, mode
+        self.n, self.mode, self.n_global = n, mode, global_count
         self.rank = id_offset // n if n else 0
         self.world = 1
 
@@ -87,11 +87,11 @@ class Context:
 
     def stats(self):
         if self.world == 1:
-            return _shard(self.rank, self.n)
+            return _shard(self.rank, self.n_global or self.n)
         w = self.world
         s = types.SimpleNamespace(bbox=[-float(w), float(w), -(2.0 * w - 1.0), 2.0 * w - 1.0],
                                   kinetic_energy=sum(0.5 * (r + 1.0) for r in range(w)),
-                                  particles=self.n * w, respawned=sum(range(w)), step=400)
+                                  particles=self.n_global or self.n * w, respawned=sum(range(w)), step=400)
         if os.environ.get("RPS_STUB_BAD_STATS") == "1":
             s.particles += 1
         return s

@@ -11,7 +11,8 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BENCH = os.path.join(ROOT, "bench.py")
-ARGS = ["--steps", "20", "--warmup", "2", "--particles", "4096", "--no-cpu-baseline", "--sph-n", "0", "--no-configs"]
+ARGS = ["--steps", "20", "--warmup", "2", "--no-cpu-baseline", "--sph-n", "0", "--no-configs"]
+WEAK = ["--particles", "4096"]
 
 
 def _run(extra, env_extra=None, timeout=240):
@@ -28,12 +29,13 @@ def _run(extra, env_extra=None, timeout=240):
 
 
 def test_gpus2_starts_two_ranks():
-    p, lines = _run(["--gpus", "2", "--allpairs-n", "8192"])
+    p, lines = _run(WEAK + ["--gpus", "2", "--allpairs-n", "8192"])
     assert p.returncode == 0, p.stderr[-3000:]
     assert len(lines) == 1, p.stdout  # rank 0 prints the one line
     line = lines[0]
     assert line["n_gpus"] == 2
     assert line["config"]["global_particles"] == 2 * 4096
+    assert line["scaling"] == "weak"
     assert line["value"] > 0 and line["steps"] == 20
     st = line["stats"]
     assert st["ranks"] == 2 and st["particles"] == 2 * 4096
@@ -43,27 +45,54 @@ def test_gpus2_starts_two_ranks():
 
 
 def test_single_process_defaults_to_one_gpu():
-    p, lines = _run(["--allpairs-n", "0"])
+    p, lines = _run(WEAK + ["--allpairs-n", "0"])
     assert p.returncode == 0, p.stderr[-3000:]
     assert lines[0]["n_gpus"] == 1
 
 
+@pytest.mark.parametrize("gpus", [1, 2])
+def test_strong_default_is_the_metric_config(gpus):
+    """Without --particles the headline is BASELINE's metric configuration at every N: 1e8
+    particles in all, split into contiguous shards; value counts the global particles."""
+    p, lines = _run(["--gpus", str(gpus), "--allpairs-n", "0", "--export-reps", "0"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = lines[0]
+    assert line["scaling"] == "strong" and line["n_gpus"] == gpus
+    assert line["config"]["global_particles"] == 10 ** 8
+    assert line["config"]["particles_per_gpu"] == 10 ** 8 // gpus
+    assert line["config"]["workload"].startswith("C3-1e8-")
+    assert line["stats"]["particles"] == 10 ** 8
+    assert abs(line["value"] - 1e8 * 20 / (line["ms_per_step"] * 20e-3)) <= 1e-6 * line["value"]
+    rf = line["roofline"]
+    assert rf["frac"] <= 1.0 and rf["bytes_per_launch"] == pytest.approx(32.03 * 10 ** 8 / gpus)
+    assert rf["achieved"] == pytest.approx(rf["bytes_per_launch"] / (rf["avg_kernel_ms"] * 1e-3) / 1e9)
+
+
+def test_strong_ragged_split():
+    """A global count that does not divide: shards [r*G/W, (r+1)*G/W), the line reports the
+    largest shard and all G particles."""
+    p, lines = _run(["--gpus", "2", "--global-particles", "8193", "--allpairs-n", "0", "--export-reps", "0"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = lines[0]
+    assert line["config"]["global_particles"] == 8193 and line["config"]["particles_per_gpu"] == 4097
+
+
 def test_launcher_world_must_match_gpus():
     env = {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0", "MASTER_PORT": "29631"}
-    p, lines = _run(["--gpus", "2", "--allpairs-n", "0"], env)
+    p, lines = _run(WEAK + ["--gpus", "2", "--allpairs-n", "0"], env)
     assert p.returncode == 2 and not lines
     assert "--gpus 2" in p.stderr
 
 
 def test_stats_mismatch_fails():
-    p, lines = _run(["--gpus", "2", "--allpairs-n", "0"], {"RPS_STUB_BAD_STATS": "1"})
+    p, lines = _run(WEAK + ["--gpus", "2", "--allpairs-n", "0"], {"RPS_STUB_BAD_STATS": "1"})
     assert p.returncode != 0
     assert lines and "mismatch" in json.dumps(lines[0]["stats"]["librps_rccl_allreduce"])
 
 
 @pytest.mark.parametrize("gpus", [1, 2])
 def test_side_run_watchdog_exits_nonzero(gpus):
-    p, lines = _run(["--gpus", str(gpus), "--allpairs-n", "8192", "--allpairs-timeout", "3"],
+    p, lines = _run(WEAK + ["--gpus", str(gpus), "--allpairs-n", "8192", "--allpairs-timeout", "3"],
                     {"RPS_STUB_HANG": "nbody"})
     assert p.returncode != 0
     assert len(lines) == 1 and "watchdog" in lines[0]["allpairs"]["error"]

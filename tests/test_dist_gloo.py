@@ -41,16 +41,24 @@ def _setup(rank, world, port):
     dist.init_process_group("gloo", rank=rank, world_size=world)
 
 
-def _stream_worker(rank, world, port, n_per, q):
+def _stream_worker(rank, world, port, n_per, q, n_global=0):
     _setup(rank, world, port)
+    import types
+
+    import bench
     import oracle as orc
     import rps_amd as rps
     from helpers import random_soa
 
-    cfg = rps.default_particle_config(n_per * world)
+    if n_global:  # bench.py's strong split: rank r owns [r*G/W, (r+1)*G/W)
+        n_per, lo, g = bench.shard(types.SimpleNamespace(particles=0, global_particles=n_global),
+                                   types.SimpleNamespace(rank=rank, world=world))
+        assert g == n_global
+    else:
+        lo, n_global = rank * n_per, n_per * world
+    cfg = rps.default_particle_config(n_global)
     ext = rps.headline_ext()
-    full = random_soa(n_per * world, list(cfg.screen_bounds), seed=77, life=(-0.1, 0.5))
-    lo = rank * n_per
+    full = random_soa(n_global, list(cfg.screen_bounds), seed=77, life=(-0.1, 0.5))
     mine = {k: v[lo:lo + n_per].copy() for k, v in full.items()}
     for s in range(7):
         orc.stream_step(cfg, ext, mine, s, id_offset=lo)
@@ -60,10 +68,16 @@ def _stream_worker(rank, world, port, n_per, q):
         for s in range(7):
             orc.stream_step(cfg, ext, ref, s, id_offset=0)
     ok = 1
-    for k in ("x", "y", "vx", "vy", "life"):
-        parts = [torch.zeros(n_per, dtype=torch.float32) for _ in range(world)]
-        dist.all_gather(parts, torch.from_numpy(mine[k]))
-        if rank == 0 and not np.array_equal(torch.cat(parts).numpy().view(np.uint32), ref[k].view(np.uint32)):
+    sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(sizes, torch.tensor([n_per]))
+    width = max(int(t.item()) for t in sizes)
+    for k in ("x", "y", "vx", "vy", "life"):  # shards padded to the largest for all_gather
+        parts = [torch.zeros(width, dtype=torch.float32) for _ in range(world)]
+        mine_k = np.zeros(width, np.float32)
+        mine_k[:n_per] = mine[k]
+        dist.all_gather(parts, torch.from_numpy(mine_k))
+        got = torch.cat([p[:int(n.item())] for p, n in zip(parts, sizes)]).numpy()
+        if rank == 0 and (got.size != n_global or not np.array_equal(got.view(np.uint32), ref[k].view(np.uint32))):
             ok = 0
     if rank == 0:
         q.put(ok)
@@ -150,15 +164,22 @@ def _bench_dist_worker(rank, world, port, q):
     d.close()
 
 
-def _run(fn, *args, world=2):
+def _run(fn, *args, world=2, extra=()):
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
-    mp.start_processes(fn, args=(world, _free_port(), *args, q), nprocs=world, join=True, start_method="spawn")
+    mp.start_processes(fn, args=(world, _free_port(), *args, q, *extra), nprocs=world, join=True,
+                       start_method="spawn")
     return q.get()
 
 
 def test_stream_shards_equal_unsharded_gloo():
     assert _run(_stream_worker, 3001) == 1
+
+
+def test_stream_strong_split_equals_unsharded_gloo():
+    """bench.py's default (strong) split of one global count, ragged across the two ranks,
+    equals the unsharded step bit for bit."""
+    assert _run(_stream_worker, 0, extra=(6003,)) == 1
 
 
 def test_nbody_allgather_shards_equal_unsharded_gloo():
