@@ -402,9 +402,9 @@ def sph_side(rps, args, d):
     sim_pmc = next((v for k, v in (pmc or {}).get("per_dispatch", {}).items() if k.startswith("sph_sim_kernel")), None)
     sim_traffic = sim_pmc["l2_read_bytes"] + sim_pmc["l2_write_bytes"] if sim_pmc else None
     hbm_frame = (pmc or {}).get("frame_sum_of_kernels", {}).get("hbm_bytes")
-    pow2 = n & (n - 1) == 0
+    slots = 1 << max(0, (n - 1).bit_length())  # P = next_pow2(N) (particle_buffers.rs:86)
     layout = os.environ.get("RPS_SPH_LAYOUT", "1")
-    spatial = pow2 and (layout == "2" or (layout == "1" and n >= (1 << 20)))  # rps_context.hip
+    spatial = layout == "2" or (layout == "1" and slots >= (1 << 20))  # rps_context.hip
     out = {"workload": f"SPH frame (5 passes, bitwise == oracle), {n} particles per rank, reference scatter",
            "record_layout": "cell tiles (spatial)" if spatial else "lookup order",
            "scaling": "replicas", "frames": args.sph_frames, "ms_per_frame": frame_ms,

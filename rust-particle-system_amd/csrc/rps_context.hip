@@ -53,11 +53,9 @@ struct rps_ctx {
   uint32_t P = 0;
   uint32_t sort_passes = 0, sort_launches = 0;
   uint8_t sph_batch_d = 0, sph_batch_s = 0;  // forced scan batches (0: by size)
-  SphLayoutArgs lay{};     // spatial record layout (P == N, RPS_SPH_LAYOUT != 0): arrays
+  SphLayoutArgs lay{};     // spatial record layout (RPS_SPH_LAYOUT, P >= 2^20 by default): arrays
   uint32_t cell_cap = 0;   // their cell capacity (0: no layout)
   bool layout_last = false;  // the last active frame used the layout (slot records in storage order)
-  uint32_t* longq_cnt = nullptr;  // the long-scan queue's two counters (SphSlots::longq; P != N)
-  uint32_t longq_par = 0;         // which of them the next active frame appends to
   bool last_frame_active = false;  // the most recent frame ran passes 4-5 (rps_sph_frame_cost)
   unsigned long long* d_count = nullptr;  // rps_sph_frame_cost's per-workgroup counts (SPH)
   // Slot-resident state (layout frames): after a layout frame st holds the
@@ -492,11 +490,7 @@ int sph_frame_begin(rps_ctx* ctx, bool layout) {
 int step_sph_sim(rps_ctx* ctx, bool layout, const SphGrid& g) {
   ctx->layout_last = layout;
   if (layout) ctx->lay.g = g;
-  if (ctx->sl.longq) {  // this frame's queue counter, and the one its density pass zeroes
-    ctx->sl.longq_n = ctx->longq_cnt + ctx->longq_par;
-    ctx->sl.longq_next = ctx->longq_cnt + (ctx->longq_par ^ 1u);
-    ctx->longq_par ^= 1u;
-  }
+  ++ctx->sl.owner_epoch;  // this active frame's owner claims (SphSlots::owner)
   SphBuffers b = sph_buffers(ctx);
   if (layout)
     RPS_HIP(ctx, launch_sph_layout_pre(b, ctx->stream));
@@ -507,7 +501,7 @@ int step_sph_sim(rps_ctx* ctx, bool layout, const SphGrid& g) {
   RPS_HIP(ctx, launch_sph_sim(b, ctx->stream));
   rc = prof_end(ctx);
   if (rc) return rc;
-  if (layout) {  // the sim wrote st in this frame's slot order and the next bin entries
+  if (layout && ctx->P == ctx->n) {  // the sim wrote st in this frame's slot order and the next bin entries
     ctx->resident = true;
     ctx->keys_valid = true;
   }
@@ -632,24 +626,24 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     slots.push_back({(void**)&ctx->sl.cur_s, align_up(P * sizeof(f2), 256)});
     slots.push_back({(void**)&ctx->ends, align_up(n * sizeof(uint32_t), 256)});
     slots.push_back({(void**)&ctx->sl.nbr_mask, align_up(2 * P * sizeof(uint64_t), 256)});
-    if (P != n) slots.push_back({(void**)&ctx->sl.owner, align_up(n * sizeof(uint32_t), 256)});
+    if (P != n) slots.push_back({(void**)&ctx->sl.owner, align_up(n * sizeof(uint64_t), 256)});
     // Long scans one per wave (rps_kernels.hip, kLongScan): P != N, where the reference's pad
     // hazard grows long duplicate runs.  RPS_SPH_LONGQ=0 keeps them in their lanes (A/B).
     if (P != n && env_int("RPS_SPH_LONGQ", 1) != 0) {
-      slots.push_back({(void**)&ctx->sl.longq, align_up(P * sizeof(uint32_t), 256)});
-      slots.push_back({(void**)&ctx->longq_cnt, 256});
+      slots.push_back({(void**)&ctx->sl.longq, align_up((P + 1) * sizeof(uint4), 256)});
+      slots.push_back({(void**)&ctx->sl.longq_n, 256});
     }
     slots.push_back({(void**)&ctx->lookup, align_up((size_t)ctx->P * sizeof(uint2), 256)});
     slots.push_back({(void**)&ctx->offsets, align_up(n * sizeof(uint32_t), 256)});
     slots.push_back({(void**)&ctx->dens, align_up(n * sizeof(f2), 256)});
     slots.push_back({(void**)&ctx->pred, align_up(n * sizeof(f2), 256)});
     slots.push_back({(void**)&ctx->d_count, align_up(2 * sph_count_blocks(ctx->P) * sizeof(unsigned long long), 256)});
-    // Spatial record layout (rps_kernels.hip): RPS_SPH_LAYOUT=0 off, 1 (default) from 2^20
-    // particles, where it is measured faster (with slot-resident state, same box: 2^20 frame
+    // Spatial record layout (rps_kernels.hip): RPS_SPH_LAYOUT=0 off, 1 (default) from P = 2^20
+    // slots, where it is measured faster (with slot-resident state, same box: 2^20 frame
     // 0.3442 -> 0.3230 ms, 2^19 0.2274 -> 0.2269, 2^18 0.1429 -> 0.1458 slower),
-    // 2 at any P == N.
+    // 2 at any size.  With P != N (pad slots) the state stays in particle order.
     const int lay_mode = env_int("RPS_SPH_LAYOUT", 1);
-    if (P == n && (lay_mode == 2 || (lay_mode == 1 && n >= (1u << 20)))) {
+    if (lay_mode == 2 || (lay_mode == 1 && P >= (1u << 20))) {
       // Up to 1 cell per particle (the bench's viewport, like the reference default, has
       // ~0.52), and at least the reference's default 1920 x 1080 viewport (~27 000 cells).
       ctx->cell_cap = (uint32_t)std::max<size_t>(n, 1u << 16);
@@ -661,9 +655,11 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
       slots.push_back({(void**)&ctx->lay.out_runs, align_up(n * sizeof(uint2), 256)});
       slots.push_back({(void**)&ctx->lay.keybits, align_up((n / 32 + 1) * sizeof(uint32_t), 256)});
       slots.push_back({(void**)&ctx->lay.n_out, 256});
-      slots.push_back({(void**)&ctx->st_alt, align_up(n * sizeof(f4), 256)});
-      slots.push_back({(void**)&ctx->idx_alt, align_up(P * sizeof(uint32_t), 256)});
-      slots.push_back({(void**)&ctx->bin_next, align_up(n * sizeof(uint2), 256)});
+      if (P == n) {  // slot-resident state (stale pad payloads would name old slots otherwise)
+        slots.push_back({(void**)&ctx->st_alt, align_up(n * sizeof(f4), 256)});
+        slots.push_back({(void**)&ctx->idx_alt, align_up(P * sizeof(uint32_t), 256)});
+        slots.push_back({(void**)&ctx->bin_next, align_up(n * sizeof(uint2), 256)});
+      }
     }
   }
   if (ctx->mode == RPS_MODE_NBODY) {

@@ -107,18 +107,20 @@ struct SphSlots {
   uint32_t* idx_s;  // P particle index (self-skip, wgsl:295 / :365)
   f2* cur_s;     // P current positions (Euler base)
   uint64_t* nbr_mask;  // 2 x P: bit f set <=> flat entry f of the nine runs is within the radius
-  // P != N only (else nullptr): owner[i] = the lowest slot holding particle i in the last active
-  // frame (reset before its predict pass, claimed by atomicMin in it).  Pad
-  // slots repeat particles; a repeat computes exactly its owner's values, so the
-  // sim runs on owner slots only, and slots >= N (never a neighbour entry) skip the density too.
-  uint32_t* owner;
+  // P != N only (else nullptr): owner[i] = {owner_epoch, ~slot} of the lowest slot holding
+  // particle i in the last active frame (claimed by atomicMax in its predict pass; an older
+  // epoch loses, so no reset).  Pad slots repeat particles; a repeat computes
+  // exactly its owner's values, so the sim runs on owner slots only, and slots >= N (never a
+  // neighbour entry) skip the density too.
+  uint64_t* owner;
+  uint32_t owner_epoch;  // the last active frame's (1, 2, ...; the arena's zeros are epoch 0)
   // P != N only (else nullptr): the slots whose nine runs hold more than kLongScan entries,
-  // appended by the density pass and computed one per wave by the long-scan kernels
-  // (rps_kernels.hip).  longq_n counts this active frame's entries; longq_next is the other of
-  // two counters, which the density pass zeroes for the next active frame.
-  uint32_t* longq;
+  // appended by the density pass as {slot + 1, predicted x, y bits, 0} and computed one per
+  // wave by the long-scan kernels (rps_kernels.hip).  P + 1 entries, {0, ...} past the last
+  // one (the sim's long kernel clears what it read); longq_n is the append counter, which the
+  // sim's long kernel zeroes for the next active frame.
+  uint4* longq;
   uint32_t* longq_n;
-  uint32_t* longq_next;
 };
 // Cell range of the spatial record layout (rps_kernels.hip): cells [cx_lo, cx_lo + w) x
 // [cy_lo, cy_lo + h), enumerated in 8 x 8 tiles, tw tiles per row; cells = tiles x 64.

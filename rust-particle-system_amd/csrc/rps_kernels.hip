@@ -1416,6 +1416,19 @@ __constant__ int32_t kGridOff[9][2] = {{-1, -1}, {-1, 0}, {-1, 1}, {0, -1}, {0, 
 // densities buffers are not written on the hot path; launch_sph_debug_views rebuilds them
 // from the slot records on readback.  Pad slots repeat some particle and
 // write identical values.
+// Slot ownership (P != N, SphSlots::owner): {epoch, ~slot} in one u64 per particle, claimed by
+// atomicMax, so the lowest slot of the current active frame wins and an entry of an older
+// frame loses to any claim without a reset pass (a memset launch per frame, 4.7 us at 50 000).
+__device__ __forceinline__ uint64_t owner_tag(const SphSlots& sl, uint32_t t) {
+  return ((uint64_t)sl.owner_epoch << 32) | (uint64_t)(0xFFFFFFFFu - t);
+}
+__device__ __forceinline__ void owner_claim(const SphSlots& sl, uint32_t i, uint32_t t) {
+  atomicMax(reinterpret_cast<unsigned long long*>(sl.owner + i), (unsigned long long)owner_tag(sl, t));
+}
+__device__ __forceinline__ bool owner_is(const SphSlots& sl, uint32_t i, uint32_t t) {
+  return sl.owner[i] == owner_tag(sl, t);
+}
+
 // apply_gravity (wgsl:397-400) and the prediction (:402-405) of particle i into slot u.
 // `e` is the sort payload: the particle index, or with slot-resident state the particle's slot
 // in st (its index then idx_prev[e]).
@@ -1424,6 +1437,7 @@ __device__ __forceinline__ void predict_slot(const rps_config* __restrict__ cfg,
                                              const uint32_t* __restrict__ idx_prev = nullptr) {
   const f4 s = st[e];
   const uint32_t i = idx_prev ? idx_prev[e] : e;
+  if (sl.owner) owner_claim(sl, i, u);  // P != N: the lowest slot of particle i owns it
   const float dt = cfg->fixed_delta_time;
   const float qx = s[2] + 0.0f * dt;  // apply_gravity, wgsl:397-400
   const float qy = s[3] + (-cfg->gravity) * dt;
@@ -1450,7 +1464,6 @@ __global__ __launch_bounds__(kBlock) void sph_predict_kernel(const rps_config* _
     if (e.x != prev) offsets[e.x] = t;
     if (e.x != next || t + 1u == n_offsets) ends[e.x] = t + 1u;
   }
-  if (sl.owner) atomicMin(&sl.owner[e.y], t);
   predict_slot(cfg, st, sl, t, e.y);
 }
 
@@ -1579,7 +1592,7 @@ __device__ __forceinline__ float readlane_f(float v, uint32_t lane) {
 }
 
 // Appends v for every lane with `want` to q (one atomic per wave).
-__device__ __forceinline__ void wave_append(bool want, uint32_t* count, uint32_t* q, uint32_t v) {
+__device__ __forceinline__ void wave_append(bool want, uint32_t* count, uint4* q, uint4 v) {
   const uint64_t m = __builtin_amdgcn_ballot_w64(want);
   if (!m) return;
   const uint32_t leader = (uint32_t)__builtin_ctzll(m);
@@ -1645,7 +1658,7 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
   if (t >= p_slots) return;
   const uint32_t N = cfg->particle_count;
   if (LAYOUT && t <= N / 32u) rb.keybits[t] = 0u;  // the fixup has read it; the next runs kernel sets it
-  if (sl.owner && t >= N && sl.owner[sl.idx_s[t]] != t) return;  // a repeat no scan visits
+  if (sl.owner && t >= N && !owner_is(sl, sl.idx_s[t], t)) return;  // a repeat no scan visits
   const f2 p = sl.pp_s[t];
   const float r = cfg->smoothing_radius, r2 = r * r;
   const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
@@ -1666,9 +1679,8 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
   // them scanned whole: 2 180 entries by frame 70, the kernel's critical path).
   const bool own_finite = fabsf(p[0]) < INFINITY && fabsf(p[1]) < INFINITY;
   if (sl.longq) {  // long scans go to sph_density_long_kernel (see there)
-    if (t == 0u) *sl.longq_next = 0u;  // the next active frame's count (its last use has ended)
     const bool defer = long_scan(total, p);
-    wave_append(defer, sl.longq_n, sl.longq, t);
+    wave_append(defer, sl.longq_n, sl.longq, make_uint4(t + 1u, __float_as_uint(p[0]), __float_as_uint(p[1]), 0u));
     if (defer) return;
   }
   const bool may_stop = own_finite || total > 128u;
@@ -1701,16 +1713,17 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
 template <bool LAYOUT>
 __global__ __launch_bounds__(kBlock) void sph_density_long_kernel(const rps_config* __restrict__ cfg,
                                                                   RunBounds rb, SphSlots sl, uint32_t p_slots) {
-  const uint32_t count = *sl.longq_n;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t nw = gridDim.x * (kBlock / 64u);
   const uint32_t N = cfg->particle_count;
   const float r = cfg->smoothing_radius, r2 = r * r;
   const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
   __shared__ RunTable runs;
-  for (uint32_t k = blockIdx.x * (kBlock / 64u) + (threadIdx.x >> 6); k < count; k += nw) {
-    const uint32_t t = sl.longq[k];
-    const f2 p = sl.pp_s[t];
+  for (uint32_t k = blockIdx.x * (kBlock / 64u) + (threadIdx.x >> 6);; k += nw) {
+    const uint4 e = sl.longq[k];
+    if (!e.x) break;  // past the last entry
+    const uint32_t t = e.x - 1u;
+    const f2 p = f2{__uint_as_float(e.y), __uint_as_float(e.z)};
     // Every lane builds the slot's table in its own column: lane l then walks entries l, l + 64, ...
     const uint32_t total = nine_runs<LAYOUT>(rb, p[0], p[1], cfg->screen_bounds[1], cfg->screen_bounds[3], r, N, runs);
     RunCursor rc(runs);
@@ -1852,8 +1865,9 @@ __device__ __forceinline__ SimOwn sim_own(const rps_config* __restrict__ cfg, co
   return SimOwn{f2{own[0], own[1]}, own[2], Pn / (rho * rho), sl.idx_s[t]};
 }
 
-// Viscosity applied, Euler (wgsl:392-395), walls (:69-99) and the store of slot t's new state.
-template <bool LAYOUT>
+// Viscosity applied, Euler (wgsl:392-395), walls (:69-99) and the store of slot t's new state
+// (RESIDENT: at the slot, slot-resident state; else at the particle).
+template <bool RESIDENT>
 __device__ __forceinline__ void sim_finish(const rps_config* __restrict__ cfg, const SphSlots& sl, f4* __restrict__ st,
                                            uint2* __restrict__ bin_next, uint32_t t, uint32_t i, float qx, float qy,
                                            float wx, float wy) {
@@ -1865,7 +1879,7 @@ __device__ __forceinline__ void sim_finish(const rps_config* __restrict__ cfg, c
   float oy = c[1] + qy * dt;
   wall(cfg->screen_bounds[0], cfg->screen_bounds[1], cfg->screen_bounds[2], cfg->screen_bounds[3],
        cfg->damping_factor, ox, oy, qx, qy);
-  if (LAYOUT) {
+  if (RESIDENT) {
     // Slot-resident state: the new state at its slot (a coalesced store instead of a 16-B
     // scatter), and the next frame's bin entry of particle i (bin_key's ops on the same
     // position and config), which the next head launch reads in place of the positions.
@@ -1894,7 +1908,7 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= p_slots) return;
   const SimOwn o = sim_own(cfg, sl, t);
-  if (kPads && sl.owner[o.i] != t) return;  // a repeat: its owner slot computes the same state
+  if (kPads && !owner_is(sl, o.i, t)) return;  // a repeat: its owner slot computes the same state
   const uint32_t self = kPads ? o.i : t;
   const float dt = cfg->fixed_delta_time;
   const float r = cfg->smoothing_radius, r2 = r * r;
@@ -1939,7 +1953,7 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
     scan_masked<kScanBatch, kPads>(sl, runs, m0, m1, self, load_pv, viscosity, viscosity_nan);
   else
     scan_runs<kScanBatch, kPads>(sl, runs, 0u, total, p, r2, self, load_pv, viscosity, viscosity_nan);
-  sim_finish<LAYOUT>(cfg, sl, st, bin_next, t, o.i, qx, qy, wx, wy);
+  sim_finish<LAYOUT && !kPads>(cfg, sl, st, bin_next, t, o.i, qx, qy, wx, wy);
 }
 
 // The sim pass of the density pass's queued slots (kLongScan), one per wave: lane l evaluates
@@ -1948,7 +1962,6 @@ template <bool kPads, bool LAYOUT>
 __global__ __launch_bounds__(kBlock) void sph_sim_long_kernel(const rps_config* __restrict__ cfg,
                                                               RunBounds rb, SphSlots sl, f4* __restrict__ st,
                                                               uint2* __restrict__ bin_next) {
-  const uint32_t count = *sl.longq_n;
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t nw = gridDim.x * (kBlock / 64u);
   const float dt = cfg->fixed_delta_time;
@@ -1956,23 +1969,33 @@ __global__ __launch_bounds__(kBlock) void sph_sim_long_kernel(const rps_config* 
   const uint32_t N = cfg->particle_count;
   const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
   const float vn = cfg->viscocity_kernel_norm;
+  if (blockIdx.x == 0u && threadIdx.x == 0u) *sl.longq_n = 0u;  // the density pass's appends are done
   __shared__ RunTable runs;
-  for (uint32_t k = blockIdx.x * (kBlock / 64u) + (threadIdx.x >> 6); k < count; k += nw) {
-    const uint32_t t = sl.longq[k];
-    const SimOwn o = sim_own(cfg, sl, t);
-    if (kPads && sl.owner[o.i] != t) continue;  // a repeat (wave-uniform)
-    const uint32_t self = kPads ? o.i : t;
-    const f2 p = o.p;
+  for (uint32_t k = blockIdx.x * (kBlock / 64u) + (threadIdx.x >> 6);; k += nw) {
+    const uint4 e = sl.longq[k];
+    if (!e.x) break;  // past the last entry
+    if (lane == 0u) sl.longq[k].x = 0u;  // cleared for the next active frame
+    const uint32_t t = e.x - 1u;
+    const f2 p = f2{__uint_as_float(e.y), __uint_as_float(e.z)};
     const uint32_t total = nine_runs<LAYOUT>(rb, p[0], p[1], cfg->screen_bounds[1], cfg->screen_bounds[3], r, N, runs);
+    const SimOwn o = sim_own(cfg, sl, t);
+    const f4 own_pv = sl.rec_pv[t];
+    if (kPads && !owner_is(sl, o.i, t)) continue;  // a repeat (wave-uniform)
+    const uint32_t self = kPads ? o.i : t;
     // The entries of both scans: within the radius and not the particle itself (scan_runs);
-    // kLongSub per lane in flight, entry f = f0 + 64 u + lane.
-    const auto gather = [&](RunCursor& rc, uint32_t f0, const f4* rec, f4 (&q)[kLongSub], bool (&in)[kLongSub]) {
+    // kLongSub per lane in flight, entry f = f0 + 64 u + lane.  Both records of a chunk are
+    // gathered together; the viscosity terms need the pressure sums, so a list longer than one
+    // chunk gathers its velocity records again after the pressure scan.
+    const bool one = total <= 64u * kLongSub;
+    const auto gather = [&](RunCursor& rc, uint32_t f0, const f4* rec, f4 (&q)[kLongSub], f4 (&qv)[kLongSub],
+                            bool (&in)[kLongSub], bool both) {
       uint32_t j[kLongSub], qi[kLongSub];
 #pragma unroll
       for (uint32_t u = 0; u < kLongSub; ++u) j[u] = rc.slot_skip(min(f0 + 64u * u + lane, total - 1u));
 #pragma unroll
       for (uint32_t u = 0; u < kLongSub; ++u) {
         q[u] = rec[j[u]];
+        if (both) qv[u] = sl.rec_pv[j[u]];
         qi[u] = kPads ? sl.idx_s[j[u]] : j[u];
       }
 #pragma unroll
@@ -1981,17 +2004,18 @@ __global__ __launch_bounds__(kBlock) void sph_sim_long_kernel(const rps_config* 
         in[u] = f0 + 64u * u + lane < total && qi[u] != self && !(dx * dx + dy * dy > r2);
       }
     };
+    f4 qv[kLongSub];
+    bool in1[kLongSub];
     float fx = 0.0f, fy = 0.0f;
     {
       RunCursor rc(runs);
       for (uint32_t f0 = 0; f0 < total && !(fx != fx && fy != fy); f0 += 64u * kLongSub) {
         f4 q[kLongSub];
-        bool in[kLongSub];
-        gather(rc, f0, sl.rec_pd, q, in);
+        gather(rc, f0, sl.rec_pd, q, qv, in1, one);
 #pragma unroll
         for (uint32_t u = 0; u < kLongSub; ++u) {
           const f4 w = pressure_terms(q[u], p, o.P_rho2, o.Pn_rho2, r, dn, ndn);
-          for (uint64_t m = __builtin_amdgcn_ballot_w64(in[u]); m; m &= m - 1u) {
+          for (uint64_t m = __builtin_amdgcn_ballot_w64(in1[u]); m; m &= m - 1u) {
             const uint32_t b = (uint32_t)__builtin_ctzll(m);
             fx = fx + readlane_f(w[0], b);
             fy = fy + readlane_f(w[1], b);
@@ -2001,29 +2025,33 @@ __global__ __launch_bounds__(kBlock) void sph_sim_long_kernel(const rps_config* 
         }
       }
     }
-    const f4 own_pv = sl.rec_pv[t];
     const float qx = own_pv[2] + fx * dt;
     const float qy = own_pv[3] + fy * dt;
     float wx = 0.0f, wy = 0.0f;
-    {
+    const auto visc = [&](const f4 (&q)[kLongSub], const bool (&in)[kLongSub]) {
+#pragma unroll
+      for (uint32_t u = 0; u < kLongSub; ++u) {
+        const float kw = viscosity_weight(q[u], p, r, vn);
+        const float tx = (q[u][2] - qx) * kw, ty = (q[u][3] - qy) * kw;
+        for (uint64_t m = __builtin_amdgcn_ballot_w64(in[u]); m; m &= m - 1u) {
+          const uint32_t b = (uint32_t)__builtin_ctzll(m);
+          wx = wx + readlane_f(tx, b);
+          wy = wy + readlane_f(ty, b);
+        }
+      }
+    };
+    if (one) {
+      visc(qv, in1);  // rec_pv's position is rec_pd's: the same entries pass the test
+    } else {
       RunCursor rc(runs);
       for (uint32_t f0 = 0; f0 < total && !(wx != wx && wy != wy); f0 += 64u * kLongSub) {
         f4 q[kLongSub];
         bool in[kLongSub];
-        gather(rc, f0, sl.rec_pv, q, in);
-#pragma unroll
-        for (uint32_t u = 0; u < kLongSub; ++u) {
-          const float kw = viscosity_weight(q[u], p, r, vn);
-          const float tx = (q[u][2] - qx) * kw, ty = (q[u][3] - qy) * kw;
-          for (uint64_t m = __builtin_amdgcn_ballot_w64(in[u]); m; m &= m - 1u) {
-            const uint32_t b = (uint32_t)__builtin_ctzll(m);
-            wx = wx + readlane_f(tx, b);
-            wy = wy + readlane_f(ty, b);
-          }
-        }
+        gather(rc, f0, sl.rec_pv, q, qv, in, false);
+        visc(q, in);
       }
     }
-    if (lane == 0u) sim_finish<LAYOUT>(cfg, sl, st, bin_next, t, o.i, qx, qy, wx, wy);
+    if (lane == 0u) sim_finish<LAYOUT && !kPads>(cfg, sl, st, bin_next, t, o.i, qx, qy, wx, wy);
   }
 }
 
@@ -2035,7 +2063,7 @@ __global__ __launch_bounds__(kBlock) void sph_debug_views_kernel(SphSlots sl, f2
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= p_slots) return;
   const uint32_t i = sl.idx_s[t];
-  if (sl.owner && sl.owner[i] != t) return;  // repeats may have skipped the density pass
+  if (sl.owner && !owner_is(sl, i, t)) return;  // repeats may have skipped the density pass
   pred[i] = sl.pp_s[t];
   dens[i] = sl.dens_s[t];
 }
@@ -2290,7 +2318,7 @@ __global__ __launch_bounds__(kBlock) void sph_layout_write_kernel(SphLayoutArgs 
                                                                   const uint2* __restrict__ lookup,
                                                                   const f4* __restrict__ st,
                                                                   const uint32_t* __restrict__ idx_prev,
-                                                                  SphSlots sl, uint32_t N) {
+                                                                  SphSlots sl, uint32_t N, uint32_t p_slots) {
   __shared__ uint32_t lbase[kBlock], lsrc[kBlock], lidx[kRunIdx][kBlock];
   __shared__ uint8_t lcell[kSlotMap];
   const uint32_t e = blockIdx.x * kBlock + threadIdx.x;
@@ -2352,6 +2380,11 @@ __global__ __launch_bounds__(kBlock) void sph_layout_write_kernel(SphLayoutArgs 
     const uint2 run = a.out_runs[lo];
     predict_slot(cfg, st, sl, k, lookup[run.x + (k - run.y)].y, idx_prev);
   }
+  // P != N: the pad slots [N, P) (never scanned) keep lookup order after the
+  // layout's N storage slots; the density and sim passes compute only those that own their
+  // particle (one pushed out of [0, N) by stale entries).
+  for (uint32_t k = N + blockIdx.x * kBlock + threadIdx.x; k < p_slots; k += stride)
+    predict_slot(cfg, st, sl, k, lookup[k].y, idx_prev);
 }
 
 // Cells owning no run take their key's storage run from run2 (complete after the write pass).
@@ -2713,12 +2746,8 @@ static hipError_t launch_sph_density(const SphBuffers& b, hipStream_t s) {
 }
 
 hipError_t launch_sph_pre(const SphBuffers& b, hipStream_t s) {
-  // Owners are claimed by the predict pass of active frames only, so after gated frames they
-  // still describe the slot records (rps_read_debug's views).
-  if (b.sl.owner) {
-    const hipError_t e = hipMemsetAsync(b.sl.owner, 0xFF, (size_t)b.n * sizeof(uint32_t), s);
-    if (e != hipSuccess) return e;
-  }
+  // Owners are claimed by the predict pass of active frames only (with the frame's epoch), so
+  // after gated frames they still describe the slot records (rps_read_debug's views).
   hipLaunchKernelGGL(sph_predict_kernel, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg, b.lookup, b.st,
                      b.sl, b.p, b.offsets, b.ends, b.n);
   const hipError_t e = hipGetLastError();
@@ -2759,7 +2788,7 @@ hipError_t launch_sph_layout_pre(const SphBuffers& b, hipStream_t s) {
   hipLaunchKernelGGL(sph_layout_scan_kernel, dim3(1), dim3(1024), 0, s, a, b.lookup, nparts);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(sph_layout_write_kernel, dim3(nparts), dim3(kBlock), 0, s, a, b.cfg, b.lookup, b.st,
-                     b.resident ? b.idx_prev : nullptr, b.sl, b.n);
+                     b.resident ? b.idx_prev : nullptr, b.sl, b.n, b.p);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(sph_layout_fixup_kernel, dim3(nparts), dim3(kBlock), 0, s, a, b.n);
   if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -2769,8 +2798,11 @@ hipError_t launch_sph_layout_pre(const SphBuffers& b, hipStream_t s) {
 hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s) {
   const RunBounds rb = run_bounds(b);
 #define RPS_SIM(B)                                                                                  \
-  if (b.layout)                                                                                     \
+  if (b.layout && b.p == b.n)                                                                       \
     hipLaunchKernelGGL((sph_sim_kernel<B, false, true>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s, \
+                       b.cfg, rb, b.sl, b.st, b.bin_next, b.p);                                           \
+  else if (b.layout)                                                                                \
+    hipLaunchKernelGGL((sph_sim_kernel<B, true, true>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s, \
                        b.cfg, rb, b.sl, b.st, b.bin_next, b.p);                                           \
   else if (b.p == b.n)                                                                              \
     hipLaunchKernelGGL((sph_sim_kernel<B, false, false>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s, \
@@ -2789,8 +2821,8 @@ hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s) {
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const dim3 g(long_blocks(b.p));
-    if (b.layout)
-      hipLaunchKernelGGL((sph_sim_long_kernel<false, true>), g, dim3(kBlock), 0, s, b.cfg, rb, b.sl, b.st, b.bin_next);
+    if (b.layout)  // long scans exist only with P != N
+      hipLaunchKernelGGL((sph_sim_long_kernel<true, true>), g, dim3(kBlock), 0, s, b.cfg, rb, b.sl, b.st, b.bin_next);
     else if (b.p == b.n)
       hipLaunchKernelGGL((sph_sim_long_kernel<false, false>), g, dim3(kBlock), 0, s, b.cfg, rb, b.sl, b.st, b.bin_next);
     else

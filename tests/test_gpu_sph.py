@@ -359,6 +359,48 @@ def test_sph_spatial_layout_forced(gpu, orc, monkeypatch, case):
     _frames_vs_oracle(rps, orc, n, soa, cfg, 4, cfg_at=cfg_at)
 
 
+@pytest.mark.parametrize("n", [3, 17, 100, 3000, 16383, 40000])
+def test_sph_spatial_layout_ragged(gpu, orc, monkeypatch, n):
+    """The layout forced at non-power-of-two N (P = next_pow2(N) > N): the pad entries sort in
+    and only [0, N) is scanned, so the layout's storage covers the N scanned
+    slots in cell order and the P - N pad slots after them in lookup order; the lowest slot of
+    each particle owns it (its sim), particles pushed past N included.  Six frames bitwise."""
+    rps = gpu
+    monkeypatch.setenv("RPS_SPH_LAYOUT", "2")
+    cfg = rps.default_particle_config(n, gravity=100.0)
+    _frames_vs_oracle(rps, orc, n, _blob(n, 90 + n, spread=max(15.0, (n ** 0.5) * 2.0)), cfg, 6)
+
+
+@pytest.mark.parametrize("layout", ["2", "0"])
+def test_sph_reference_default_long_runs(gpu, orc, monkeypatch, layout):
+    """The reference default (N = 50 000, its scatter and viewport) over 14 active frames:
+    the stale pad duplicates grow runs of 150+ entries near key N, and particles turn NaN and
+    pile into the key-0 run, so scans exceed 128 entries; those are walked one slot per wave
+    (rps_kernels.hip, kLongScan).  With and without the spatial layout, every frame bitwise."""
+    rps = gpu
+    monkeypatch.setenv("RPS_SPH_LAYOUT", layout)
+    n = 50000
+    cfg = rps.default_particle_config(n)
+    parts = rps.setup_particles_scatter(cfg, n, seed=1)
+    soa = dict(x=parts["position"][:, 0].copy(), y=parts["position"][:, 1].copy(),
+               vx=parts["velocity"][:, 0].copy(), vy=parts["velocity"][:, 1].copy())
+    _frames_vs_oracle(rps, orc, n, soa, cfg, 14, download_at={5, 9, 13})
+
+
+def test_sph_layout_one_million(gpu, orc):
+    """BASELINE C2's literal size, N = 10^6 (P = 2^20): the default selects the spatial layout
+    (from P = 2^20) with pad slots; the bench's viewport scaled to the default density, three
+    frames bitwise."""
+    rps = gpu
+    n = 1_000_000
+    scale = (n / 50000) ** 0.5
+    cfg = rps.default_particle_config(n, screen_bounds=rps.screen_bounds_for(1920.0 * scale, 1080.0 * scale))
+    parts = rps.setup_particles_scatter(cfg, n, seed=0x5EED)
+    soa = dict(x=parts["position"][:, 0].copy(), y=parts["position"][:, 1].copy(),
+               vx=parts["velocity"][:, 0].copy(), vy=parts["velocity"][:, 1].copy())
+    _frames_vs_oracle(rps, orc, n, soa, cfg, 3)
+
+
 @pytest.mark.parametrize("layout", ["0", "2"])
 @pytest.mark.parametrize("case", ["stacked", "tiny", "huge"])
 def test_sph_division_operand_ranges(gpu, orc, monkeypatch, layout, case):
