@@ -99,6 +99,8 @@ hipError_t launch_nbody_integrate(const NbodyIntegrateArgs& a, hipStream_t s);
 // SPH (the reference's five passes).
 // Per-slot records in spatial-lookup order (slot t holds particle lookup[t].y's values), so
 // a run's entries are contiguous.  Written by the predict pass except rec_pd (density pass).
+// Scans of more entries than this are "long" (rps_kernels.hip): the masks' capacity.
+constexpr uint32_t kLongScan = 128u;
 struct SphSlots {
   f2* pp_s;      // P predicted positions                    (density scan: 8 B/entry)
   f4* rec_pv;    // P {predicted x, y, post-gravity vx, vy}  (viscosity scan)
@@ -121,6 +123,7 @@ struct SphSlots {
   // sim's long kernel zeroes for the next active frame.
   uint4* longq;
   uint32_t* longq_n;
+  uint32_t long_min;  // a scan of more entries than this is long (kLongScan; RPS_SPH_LONG_MIN)
 };
 // Cell range of the spatial record layout (rps_kernels.hip): cells [cx_lo, cx_lo + w) x
 // [cy_lo, cy_lo + h), enumerated in 8 x 8 tiles, tw tiles per row; cells = tiles x 64.

@@ -1581,10 +1581,9 @@ struct RunCursor {
 // same additions in the same order as in its own lane.
 // A particle whose own position is not finite stays in its lane: its sums are NaN from its
 // first entry on, and both scans stop after one batch.
-constexpr uint32_t kLongScan = 128u;
 constexpr uint32_t kLongSub = 4;  // entries per lane in flight in the long-scan kernels (256 per wave)
-__device__ __forceinline__ bool long_scan(uint32_t total, f2 p) {
-  return total > kLongScan && fabsf(p[0]) < INFINITY && fabsf(p[1]) < INFINITY;
+__device__ __forceinline__ bool long_scan(const SphSlots& sl, uint32_t total, f2 p) {
+  return total > sl.long_min && fabsf(p[0]) < INFINITY && fabsf(p[1]) < INFINITY;
 }
 
 __device__ __forceinline__ float readlane_f(float v, uint32_t lane) {
@@ -1679,7 +1678,7 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
   // them scanned whole: 2 180 entries by frame 70, the kernel's critical path).
   const bool own_finite = fabsf(p[0]) < INFINITY && fabsf(p[1]) < INFINITY;
   if (sl.longq) {  // long scans go to sph_density_long_kernel (see there)
-    const bool defer = long_scan(total, p);
+    const bool defer = long_scan(sl, total, p);
     wave_append(defer, sl.longq_n, sl.longq, make_uint4(t + 1u, __float_as_uint(p[0]), __float_as_uint(p[1]), 0u));
     if (defer) return;
   }
@@ -1920,7 +1919,7 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
   const uint32_t total = nine_runs<LAYOUT>(rb, p[0], p[1], cfg->screen_bounds[1],
                                    cfg->screen_bounds[3], r, N, runs);
   const bool masked = total <= 128u;
-  if (sl.longq && long_scan(total, p)) return;  // queued by the density pass
+  if (sl.longq && long_scan(sl, total, p)) return;  // queued by the density pass
   const uint64_t m0 = masked ? sl.nbr_mask[t] : 0u, m1 = masked ? sl.nbr_mask[p_slots + t] : 0u;
   float fx = 0.0f, fy = 0.0f;
   const auto load_pd = [&](uint32_t j) { return sl.rec_pd[j]; };

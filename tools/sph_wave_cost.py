@@ -107,6 +107,14 @@ def analyse(n, frames):
                      "top_waves": [int(v) for v in np.sort(wmax)[-8:]],
                      "cost_in_top_1pct_waves": float(np.sort(wmax)[-max(1, len(wmax) // 100):].sum() / wmax.sum())}
     out["lanes_over_128"] = int(((total > 128) & live_sim).sum())
+    long_ = (total > 128) & own_fin  # the long-scan queue (rps_kernels.hip kLongScan)
+    out["long_queue_density"] = int((long_ & live_den).sum())
+    out["long_queue_sim_owners"] = int((long_ & live_sim).sum())
+    short_sim = np.where(live_sim & ~long_, sim_cost, 0).reshape(-1, 64).max(1)
+    short_den = np.where(live_den & ~long_, den_cost, 0).reshape(-1, 64).max(1)
+    out["short_wave_max"] = {"sim_max": int(short_sim.max()), "sim_p99": float(np.percentile(short_sim, 99)),
+                             "sim_mean": float(short_sim.mean()), "den_max": int(short_den.max()),
+                             "den_p99": float(np.percentile(short_den, 99)), "den_mean": float(short_den.mean())}
     # the longest sim lanes: what they scan
     top = np.argsort(np.where(live_sim, sim_cost, -1))[-6:]
     out["top_sim_lanes"] = [{"slot": int(t), "particle": int(idx[t]), "cost": int(sim_cost[t]), "total": int(total[t]),
