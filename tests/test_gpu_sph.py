@@ -371,14 +371,17 @@ def test_sph_spatial_layout_ragged(gpu, orc, monkeypatch, n):
     _frames_vs_oracle(rps, orc, n, _blob(n, 90 + n, spread=max(15.0, (n ** 0.5) * 2.0)), cfg, 6)
 
 
-@pytest.mark.parametrize("layout", ["2", "0"])
-def test_sph_reference_default_long_runs(gpu, orc, monkeypatch, layout):
+@pytest.mark.parametrize("layout,long_min", [("2", None), ("0", None), ("0", "8"), ("2", "128")])
+def test_sph_reference_default_long_runs(gpu, orc, monkeypatch, layout, long_min):
     """The reference default (N = 50 000, its scatter and viewport) over 14 active frames:
     the stale pad duplicates grow runs of 150+ entries near key N, and particles turn NaN and
-    pile into the key-0 run, so scans exceed 128 entries; those are walked one slot per wave
-    (rps_kernels.hip, kLongScan).  With and without the spatial layout, every frame bitwise."""
+    pile into the key-0 run, so scans exceed 64 / 128 entries; those are walked one slot per
+    wave (rps_kernels.hip, SphSlots::long_min; 8 sends most slots there, masked ones included).
+    With and without the spatial layout, every frame bitwise."""
     rps = gpu
     monkeypatch.setenv("RPS_SPH_LAYOUT", layout)
+    if long_min:
+        monkeypatch.setenv("RPS_SPH_LONG_MIN", long_min)
     n = 50000
     cfg = rps.default_particle_config(n)
     parts = rps.setup_particles_scatter(cfg, n, seed=1)
