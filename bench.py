@@ -399,6 +399,7 @@ def sph_side(rps, args, d):
     # Measured traffic (PMC, the bench workload at 2^22; profiles/pmc_traffic.json): the sim
     # kernel's L1 -> L2 request bytes, and every SPH kernel's memory-side bytes per frame.
     pmc = pmc_sph() if n == 1 << 22 else None
+    pmc_src = f"profiles/pmc_traffic.json 'SPH-2^22-frame' (round {pmc.get('round')}; not this run)" if pmc else None
     sim_pmc = next((v for k, v in (pmc or {}).get("per_dispatch", {}).items() if k.startswith("sph_sim_kernel")), None)
     sim_traffic = sim_pmc["l2_read_bytes"] + sim_pmc["l2_write_bytes"] if sim_pmc else None
     hbm_frame = (pmc or {}).get("frame_sum_of_kernels", {}).get("hbm_bytes")
@@ -414,6 +415,7 @@ def sph_side(rps, args, d):
                         "unit": "GB/s", "frac": sim_gbps / L2_PEAK_GBPS, "traffic": sim_traffic,
                         "traffic_gbps": sim_traffic / (sim_ms * 1e-3) / 1e9 if sim_traffic else None,
                         "traffic_frac": sim_traffic / (sim_ms * 1e-3) / 1e9 / L2_PEAK_GBPS if sim_traffic else None,
+                        "traffic_source": pmc_src,
                         "algorithmic_bytes_per_launch": cost["sim_bytes"],
                         "scanned_entries_per_particle": cost["scanned_entries"] / cost["slots"],
                         "within_radius_per_particle": cost["within_entries"] / cost["slots"],
@@ -424,7 +426,7 @@ def sph_side(rps, args, d):
                                 "the same peak"},
            "frame_cost": {"bytes": cost["frame_bytes"], "gbps": cost["frame_bytes"] / (frame_ms * 1e-3) / 1e9,
                           "frac_of_l2": cost["frame_bytes"] / (frame_ms * 1e-3) / 1e9 / L2_PEAK_GBPS,
-                          "hbm_bytes_measured": hbm_frame,
+                          "hbm_bytes_measured": hbm_frame, "hbm_bytes_source": pmc_src,
                           "hbm_gbps_measured": hbm_frame / (frame_ms * 1e-3) / 1e9 if hbm_frame else None,
                           "hbm_frac_measured": hbm_frame / (frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS if hbm_frame else None,
                           "sort_launches": cost["sort_launches"]}}

@@ -536,9 +536,9 @@ def test_sph_layout_clustered_runs(gpu, orc, monkeypatch):
     'listed' by the runs kernel.  Their lengths come from the per-key run ends and their slots'
     prediction is spread over every thread of the write kernel (round 2 walked and predicted
     each listed run on one lane, O(run length) dependent loads).  At 2^21 (a default layout
-    size) with 16 clumps of 4096 particles each inside one cell: the first frame
-    bitwise against the oracle, and the layout frame no slower than 1.5x the lookup-order
-    frame of the same state (same clumps, same scans; only the record placement differs)."""
+    size) with 16 clumps of 4096 particles each inside one cell: the first frame bitwise
+    against the oracle, with and without the layout.  (The timing comparison of the two record
+    placements on this state lives in tools/ab_sph.py, not in this correctness suite.)"""
     rps = gpu
     n = 1 << 21
     scale = (n / 50000) ** 0.5
@@ -557,22 +557,16 @@ def test_sph_layout_clustered_runs(gpu, orc, monkeypatch):
         soa["x"][sl] = (cx + g.uniform(-0.2 * r, 0.2 * r, k)).astype(F)
         soa["y"][sl] = (cy + g.uniform(-0.2 * r, 0.2 * r, k)).astype(F)
     ext = rps.make_ext(shader_delay=0)
-    ms = {}
+    st = orc.SphState(n, omp=True)
+    ref = copy_soa(soa)
+    st.grid(cfg, ref)
+    st.pre(cfg, ref)
+    st.sim(cfg, ref)
     for layout in ("1", "0"):
         monkeypatch.setenv("RPS_SPH_LAYOUT", layout)
         with rps.Context(n, rps.MODE_SPH) as ctx:
             ctx.set_config(cfg, ext)
             ctx.upload_soa(soa)
             ctx.step(1)
-            if layout == "1":
-                st = orc.SphState(n, omp=True)
-                ref = copy_soa(soa)
-                st.grid(cfg, ref)
-                st.pre(cfg, ref)
-                assert_bitwise(ctx.read_debug(rps.DEBUG_DENSITIES), st.dens, "dens")
-                st.sim(cfg, ref)
-                assert_soa_bitwise(ctx.download_soa(), ref, what="clustered ")
-            ctx.upload_soa(soa)  # the same start state for both timings
-            ctx.step(2)
-            ms[layout] = ctx.time_steps(5) / 5
-    assert ms["1"] <= 1.5 * ms["0"], ms
+            assert_bitwise(ctx.read_debug(rps.DEBUG_DENSITIES), st.dens, f"dens layout={layout}")
+            assert_soa_bitwise(ctx.download_soa(), ref, what=f"clustered layout={layout} ")
