@@ -52,6 +52,7 @@ struct rps_ctx {
   f2* pred = nullptr;
   uint32_t P = 0;
   uint32_t sort_passes = 0, sort_launches = 0;
+  bool sort_fold = true;  // RPS_SPH_SORT_FOLD (rps_kernels.hip, launch_sph_sort)
   uint8_t sph_batch_d = 0, sph_batch_s = 0;  // forced scan batches (0: by size)
   SphLayoutArgs lay{};     // spatial record layout (RPS_SPH_LAYOUT, P >= 2^20 by default): arrays
   uint32_t cell_cap = 0;   // their cell capacity (0: no layout)
@@ -307,6 +308,7 @@ SphBuffers sph_buffers(rps_ctx* ctx) {
   b.lay = ctx->lay;
   b.cell_cap = ctx->cell_cap;
   b.layout = ctx->layout_last;
+  b.sort_fold = ctx->sort_fold;
   return b;
 }
 
@@ -461,7 +463,9 @@ int step_sph_grid(rps_ctx* ctx, bool active) {
 // The state back in particle order (st_alt[perm[u]] = st[u], then the buffers swap).
 int sph_canonical(rps_ctx* ctx) {
   if (!ctx->resident) return RPS_OK;
-  RPS_HIP(ctx, launch_sph_materialize(ctx->st, ctx->sl.idx_s, ctx->st_alt, (uint32_t)ctx->n, ctx->stream));
+  const SphBuffers b = sph_buffers(ctx);
+  RPS_HIP(ctx, launch_sph_materialize(b, ctx->st, ctx->sl.idx_s, ctx->st_alt, ctx->stream));
+  RPS_HIP(ctx, launch_sph_pad_unflag(b, ctx->stream));  // P != N: pad payloads back to indices
   std::swap(ctx->st, ctx->st_alt);
   set_sph_fields(ctx);
   ctx->resident = false;
@@ -501,7 +505,7 @@ int step_sph_sim(rps_ctx* ctx, bool layout, const SphGrid& g) {
   RPS_HIP(ctx, launch_sph_sim(b, ctx->stream));
   rc = prof_end(ctx);
   if (rc) return rc;
-  if (layout && ctx->P == ctx->n) {  // the sim wrote st in this frame's slot order and the next bin entries
+  if (layout) {  // the sim wrote st in this frame's slot order and the next bin entries
     ctx->resident = true;
     ctx->keys_valid = true;
   }
@@ -617,7 +621,12 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
   if (ctx->mode == RPS_MODE_SPH) {
     ctx->P = next_pow2_u32((uint32_t)n);  // spatial lookup sized next_pow2 (particle_buffers.rs:86)
     const size_t P = ctx->P;
-    slots.push_back({(void**)&ctx->st, align_up(n * sizeof(f4), 256)});
+    ctx->sort_fold = env_int("RPS_SPH_SORT_FOLD", 1) != 0;
+    const int lay_mode = env_int("RPS_SPH_LAYOUT", 1);
+    const bool lay_ok = lay_mode == 2 || (lay_mode == 1 && P >= (1u << 20));
+    // With the layout the state is slot-resident (one entry per slot: P of them)
+    const size_t st_n = lay_ok ? P : n;
+    slots.push_back({(void**)&ctx->st, align_up(st_n * sizeof(f4), 256)});
     slots.push_back({(void**)&ctx->sl.pp_s, align_up(P * sizeof(f2), 256)});
     slots.push_back({(void**)&ctx->sl.rec_pv, align_up(P * sizeof(f4), 256)});
     slots.push_back({(void**)&ctx->sl.rec_pd, align_up(P * sizeof(f4), 256)});
@@ -646,9 +655,8 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     // Spatial record layout (rps_kernels.hip): RPS_SPH_LAYOUT=0 off, 1 (default) from P = 2^20
     // slots, where it is measured faster (with slot-resident state, same box: 2^20 frame
     // 0.3442 -> 0.3230 ms, 2^19 0.2274 -> 0.2269, 2^18 0.1429 -> 0.1458 slower),
-    // 2 at any size.  With P != N (pad slots) the state stays in particle order.
-    const int lay_mode = env_int("RPS_SPH_LAYOUT", 1);
-    if (lay_mode == 2 || (lay_mode == 1 && P >= (1u << 20))) {
+    // 2 at any size.
+    if (lay_ok) {
       // Up to 1 cell per particle (the bench's viewport, like the reference default, has
       // ~0.52), and at least the reference's default 1920 x 1080 viewport (~27 000 cells).
       ctx->cell_cap = (uint32_t)std::max<size_t>(n, 1u << 16);
@@ -660,11 +668,11 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
       slots.push_back({(void**)&ctx->lay.out_runs, align_up(n * sizeof(uint2), 256)});
       slots.push_back({(void**)&ctx->lay.keybits, align_up((n / 32 + 1) * sizeof(uint32_t), 256)});
       slots.push_back({(void**)&ctx->lay.n_out, 256});
-      if (P == n) {  // slot-resident state (stale pad payloads would name old slots otherwise)
-        slots.push_back({(void**)&ctx->st_alt, align_up(n * sizeof(f4), 256)});
-        slots.push_back({(void**)&ctx->idx_alt, align_up(P * sizeof(uint32_t), 256)});
-        slots.push_back({(void**)&ctx->bin_next, align_up(n * sizeof(uint2), 256)});
-      }
+      // slot-resident state: the buffer st swaps with, the previous slot -> particle map, the
+      // sim's bin entries
+      slots.push_back({(void**)&ctx->st_alt, align_up(st_n * sizeof(f4), 256)});
+      slots.push_back({(void**)&ctx->idx_alt, align_up(P * sizeof(uint32_t), 256)});
+      slots.push_back({(void**)&ctx->bin_next, align_up(n * sizeof(uint2), 256)});
     }
   }
   if (ctx->mode == RPS_MODE_NBODY) {
@@ -959,12 +967,13 @@ int rps_read_debug(rps_ctx* ctx, int which, void* dst, uint64_t bytes) {
   }
   if (which == RPS_DEBUG_DENSITIES || which == RPS_DEBUG_PREDICTED)
     RPS_HIP(ctx, launch_sph_debug_views(sph_buffers(ctx), ctx->stream));
-  if (which == RPS_DEBUG_SPATIAL_LOOKUP && ctx->lookup_perm) {
-    // Slot-resident frame: payloads are the previous frame's slots; the reference holds
-    // particle indices.  Translated into out_runs (free between frames, P == N entries).
-    RPS_HIP(ctx, launch_sph_lookup_translate(ctx->lookup, ctx->lookup_perm, ctx->lay.out_runs, ctx->P,
-                                             ctx->stream));
-    src = ctx->lay.out_runs;
+  if (which == RPS_DEBUG_SPATIAL_LOOKUP && (ctx->lookup_perm || (ctx->resident && ctx->P != ctx->n))) {
+    // Slot-resident frame: payloads are the previous frame's slots (and, with P != N, the pads'
+    // flagged particle indices); the reference holds particle indices.  Translated into the
+    // neighbour masks' buffer (2 x P x 8 B, dead between frames).
+    uint2* scratch = reinterpret_cast<uint2*>(ctx->sl.nbr_mask);
+    RPS_HIP(ctx, launch_sph_lookup_translate(ctx->lookup, ctx->lookup_perm, scratch, ctx->P, ctx->stream));
+    src = scratch;
   }
   // A spatial-layout frame measures its runs without touching the reference's offsets:
   // bin_particles_in_grid's reset (wgsl:467) and pass 3 (wgsl:507-525) on the frame's sorted

@@ -99,6 +99,9 @@ hipError_t launch_nbody_integrate(const NbodyIntegrateArgs& a, hipStream_t s);
 // SPH (the reference's five passes).
 // Per-slot records in spatial-lookup order (slot t holds particle lookup[t].y's values), so
 // a run's entries are contiguous.  Written by the predict pass except rec_pd (density pass).
+// A sort payload with this bit set is a particle index, not a slot: the stale pad entries of a
+// layout frame with P != N (rps_kernels.hip, resolve_payload).
+constexpr uint32_t kPidFlag = 0x80000000u;
 // Scans of more entries than this are "long" (rps_kernels.hip): the masks' capacity.
 constexpr uint32_t kLongScan = 128u;
 struct SphSlots {
@@ -166,7 +169,8 @@ struct SphBuffers {
   uint32_t p;        // next_pow2(N)
   uint8_t batch_d;   // scan entries in flight per lane, density / sim pass (4, 8, 16;
   uint8_t batch_s;   //   0: by size, sph_batch); per context, RPS_SPH_BATCH[_D|_S] at create
-  bool layout;       // this frame uses the spatial record layout (lay.* valid, P == N)
+  bool layout;       // this frame uses the spatial record layout (lay.* valid)
+  bool sort_fold;    // the first two later sort stages fold their global passes into the tails
   uint32_t cell_cap; // capacity of lay.cell_info / cellrun (0: layout never available)
   SphLayoutArgs lay;
 };
@@ -196,7 +200,8 @@ hipError_t launch_sph_debug_views(const SphBuffers& b, hipStream_t s);
 // Slot-resident state: bin_next from the state (keys of the current config), the state back to
 // particle order (dst[perm[u]] = st[u]), and the sorted lookup's payloads as particle indices.
 hipError_t launch_sph_rebin(const SphBuffers& b, const uint32_t* perm, hipStream_t s);
-hipError_t launch_sph_materialize(const f4* st, const uint32_t* perm, f4* dst, uint32_t n, hipStream_t s);
+hipError_t launch_sph_materialize(const SphBuffers& b, const f4* st, const uint32_t* perm, f4* dst, hipStream_t s);
+hipError_t launch_sph_pad_unflag(const SphBuffers& b, hipStream_t s);
 hipError_t launch_sph_lookup_translate(const uint2* lookup, const uint32_t* perm, uint2* out, uint32_t p,
                                        hipStream_t s);
 

@@ -1051,8 +1051,51 @@ __device__ __forceinline__ void store_eight(uint2* tile, uint32_t t, uint2 (&v)[
 }
 
 
-template <int TLOG>
-__global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_eu(4))) void sph_sort_tail_kernel(uint2* __restrict__ lookup) {
+// The compare-swap of the reference's pass on the entries at positions pa != pb (the lower
+// position is the left one).
+__device__ __forceinline__ void cas_at(uint2& va, uint32_t pa, uint2& vb, uint32_t pb) {
+  uint2& l = pa < pb ? va : vb;
+  uint2& r = pa < pb ? vb : va;
+  if (l.x > r.x) {
+    const uint2 tmp = l;
+    l = r;
+    r = tmp;
+  }
+}
+
+// The value at position x after the first TG global passes of stage s (the flip, pairing x with
+// its mirror x ^ (2^(s+1) - 1), then for TG = 2 stride 2^(s-1)): the passes of the 2^TG entries
+// x's group spans (in TG other tiles), recomputed by every tile of the group; the launch's own
+// tile keeps its entry.  The same compare-swaps as the register-fused launch they replace.
+template <int TG>
+__device__ __forceinline__ uint2 folded_global(uint32_t x, uint32_t s, const uint2 (&e)[1 << TG]) {
+  const uint32_t m = (2u << s) - 1u;
+  if constexpr (TG == 1) {
+    uint2 a = e[0], ma = e[1];
+    cas_at(a, x, ma, x ^ m);
+    return a;
+  } else {
+    const uint32_t h = 1u << (s - 1u);
+    uint2 a = e[0], b = e[1], ma = e[2], mb = e[3];
+    cas_at(a, x, ma, x ^ m);  // flip
+    cas_at(b, x ^ h, mb, x ^ h ^ m);
+    cas_at(a, x, b, x ^ h);  // stride 2^(s-1)
+    cas_at(ma, x ^ m, mb, x ^ m ^ h);
+    return a;
+  }
+}
+template <int TG>
+__device__ __forceinline__ uint32_t folded_pos(uint32_t x, uint32_t s, int k) {
+  const uint32_t m = (2u << s) - 1u, h = TG == 2 ? 1u << (s - 1u) : 0u;
+  return (k & 1 ? (TG == 1 ? m : h) : 0u) ^ (k & 2 ? m : 0u) ^ x;
+}
+
+// TG > 0: the stage's first TG global passes folded in (stage s = TLOG + TG - 1; one launch
+// fewer per such stage: DESIGN.md §5.2).  Every tile of a group reads the others' entries, so
+// the launch reads `src` and writes `lookup` (a second buffer: the sort ping-pongs).
+template <int TLOG, int TG = 0>
+__global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_eu(4))) void sph_sort_tail_kernel(
+    uint2* __restrict__ lookup, const uint2* __restrict__ src) {
   static_assert(TLOG >= 10 && TLOG <= 13, "eight entries per thread, 128..1024 threads");
   constexpr uint32_t TILE = 1u << TLOG, NT = TILE / 8;
   __shared__ uint2 lds[TILE + TILE / 32];
@@ -1060,8 +1103,21 @@ __global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_e
   uint2* tile = lookup + (size_t)blockIdx.x * TILE;
   {  // strides TILE/2, TILE/4, TILE/8: group r = t, entries t + j * NT, straight from the lookup
     uint2 v[8];
+    if constexpr (TG == 0) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = tile[t + j * NT];
+      for (int j = 0; j < 8; ++j) v[j] = tile[t + j * NT];
+    } else {
+      constexpr uint32_t s = TLOG + TG - 1;
+      uint2 e[8][1 << TG];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t x = blockIdx.x * TILE + t + j * NT;
+#pragma unroll
+        for (int k = 0; k < (1 << TG); ++k) e[j][k] = src[folded_pos<TG>(x, s, k)];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = folded_global<TG>(blockIdx.x * TILE + t + j * NT, s, e[j]);
+    }
     group_passes<3>(v);
     const uint32_t a = padded(t);
 #pragma unroll
@@ -1432,11 +1488,30 @@ __device__ __forceinline__ bool owner_is(const SphSlots& sl, uint32_t i, uint32_
 // apply_gravity (wgsl:397-400) and the prediction (:402-405) of particle i into slot u.
 // `e` is the sort payload: the particle index, or with slot-resident state the particle's slot
 // in st (its index then idx_prev[e]).
-__device__ __forceinline__ void predict_slot(const rps_config* __restrict__ cfg, const f4* __restrict__ st,
-                                             const SphSlots& sl, uint32_t u, uint32_t e,
-                                             const uint32_t* __restrict__ idx_prev = nullptr) {
-  const f4 s = st[e];
-  const uint32_t i = idx_prev ? idx_prev[e] : e;
+// A sort payload: the particle index; in a slot-resident frame the particle's slot of the
+// previous frame (state st[slot], index idx_prev[slot]); or kPidFlag | index, a stale pad entry
+// of a layout frame with P != N (its payload rewritten as the index, since the slot it named is
+// gone), whose state sits at the particle's slot of the previous frame (bin_prev[index].y, the
+// sim's bin entry) in a resident frame and at the index otherwise.
+struct Payload {
+  uint32_t state, pid;
+};
+__device__ __forceinline__ Payload resolve_payload(uint32_t e, const uint32_t* __restrict__ idx_prev,
+                                                   const uint2* __restrict__ bin_prev) {
+  if (e & kPidFlag) {
+    const uint32_t i = e & ~kPidFlag;
+    return Payload{bin_prev ? bin_prev[i].y : i, i};
+  }
+  return Payload{e, idx_prev ? idx_prev[e] : e};
+}
+
+__device__ __forceinline__ uint32_t predict_slot(const rps_config* __restrict__ cfg, const f4* __restrict__ st,
+                                                 const SphSlots& sl, uint32_t u, uint32_t e,
+                                                 const uint32_t* __restrict__ idx_prev = nullptr,
+                                                 const uint2* __restrict__ bin_prev = nullptr) {
+  const Payload pl = resolve_payload(e, idx_prev, bin_prev);
+  const f4 s = st[pl.state];
+  const uint32_t i = pl.pid;
   if (sl.owner) owner_claim(sl, i, u);  // P != N: the lowest slot of particle i owns it
   const float dt = cfg->fixed_delta_time;
   const float qx = s[2] + 0.0f * dt;  // apply_gravity, wgsl:397-400
@@ -1446,6 +1521,7 @@ __device__ __forceinline__ void predict_slot(const rps_config* __restrict__ cfg,
   sl.rec_pv[u] = f4{px, py, qx, qy};
   sl.idx_s[u] = i;
   sl.cur_s[u] = f2{s[0], s[1]};
+  return i;
 }
 
 __global__ __launch_bounds__(kBlock) void sph_predict_kernel(const rps_config* __restrict__ cfg,
@@ -1952,7 +2028,7 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
     scan_masked<kScanBatch, kPads>(sl, runs, m0, m1, self, load_pv, viscosity, viscosity_nan);
   else
     scan_runs<kScanBatch, kPads>(sl, runs, 0u, total, p, r2, self, load_pv, viscosity, viscosity_nan);
-  sim_finish<LAYOUT && !kPads>(cfg, sl, st, bin_next, t, o.i, qx, qy, wx, wy);
+  sim_finish<LAYOUT>(cfg, sl, st, bin_next, t, o.i, qx, qy, wx, wy);
 }
 
 // The sim pass of the density pass's queued slots (kLongScan), one per wave: lane l evaluates
@@ -2050,7 +2126,7 @@ __global__ __launch_bounds__(kBlock) void sph_sim_long_kernel(const rps_config* 
         visc(q, in);
       }
     }
-    if (lane == 0u) sim_finish<LAYOUT && !kPads>(cfg, sl, st, bin_next, t, o.i, qx, qy, wx, wy);
+    if (lane == 0u) sim_finish<LAYOUT>(cfg, sl, st, bin_next, t, o.i, qx, qy, wx, wy);
   }
 }
 
@@ -2076,9 +2152,11 @@ __global__ __launch_bounds__(kBlock) void sph_debug_views_kernel(SphSlots sl, f2
 __global__ __launch_bounds__(kBlock) void sph_rebin_kernel(const rps_config* __restrict__ cfg,
                                                            const f4* __restrict__ st,
                                                            const uint32_t* __restrict__ perm,
-                                                           uint2* __restrict__ bin_next, uint32_t n) {
+                                                           uint2* __restrict__ bin_next, SphSlots sl,
+                                                           uint32_t slots) {
   const uint32_t u = blockIdx.x * kBlock + threadIdx.x;
-  if (u >= n) return;
+  if (u >= slots) return;
+  if (sl.owner && !owner_is(sl, perm[u], u)) return;  // P != N: the state sits at owner slots
   const f4 s = st[u];
   const float r = cfg->smoothing_radius;
   const int32_t cx = f32_to_i32((s[0] + cfg->screen_bounds[1]) / r);
@@ -2088,9 +2166,16 @@ __global__ __launch_bounds__(kBlock) void sph_rebin_kernel(const rps_config* __r
 // The state back in particle order.
 __global__ __launch_bounds__(kBlock) void sph_materialize_kernel(const f4* __restrict__ st,
                                                                  const uint32_t* __restrict__ perm,
-                                                                 f4* __restrict__ dst, uint32_t n) {
+                                                                 f4* __restrict__ dst, SphSlots sl,
+                                                                 uint32_t slots) {
   const uint32_t u = blockIdx.x * kBlock + threadIdx.x;
-  if (u < n) dst[perm[u]] = st[u];
+  if (u < slots && (!sl.owner || owner_is(sl, perm[u], u))) dst[perm[u]] = st[u];
+}
+// Leaving slot-resident state with P != N: the pad entries' payloads back to plain indices.
+__global__ __launch_bounds__(kBlock) void sph_pad_unflag_kernel(uint2* __restrict__ lookup, uint32_t n,
+                                                                uint32_t p) {
+  const uint32_t k = n + blockIdx.x * kBlock + threadIdx.x;
+  if (k < p) lookup[k].y &= ~kPidFlag;
 }
 // The sorted lookup with particle indices as payloads (the reference's spatial_lookup).
 __global__ __launch_bounds__(kBlock) void sph_lookup_translate_kernel(const uint2* __restrict__ lookup,
@@ -2099,7 +2184,7 @@ __global__ __launch_bounds__(kBlock) void sph_lookup_translate_kernel(const uint
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= p) return;
   const uint2 e = lookup[t];
-  out[t] = make_uint2(e.x, perm[e.y]);
+  out[t] = make_uint2(e.x, (e.y & kPidFlag) ? e.y & ~kPidFlag : perm ? perm[e.y] : e.y);
 }
 __global__ __launch_bounds__(kBlock) void sph_count_kernel(const rps_config* __restrict__ cfg,
                                                            const uint32_t* __restrict__ offsets,
@@ -2198,7 +2283,8 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* t
 // listed run with one load whatever its length.
 __global__ __launch_bounds__(kBlock) void sph_runs_kernel(SphLayoutArgs a, const rps_config* __restrict__ cfg,
                                                           const uint2* __restrict__ lookup,
-                                                          const f4* __restrict__ st, uint32_t n) {
+                                                          const f4* __restrict__ st, uint32_t n,
+                                                          const uint2* __restrict__ bin_prev) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
   const bool valid = t < n;  // every lane stays for the wave-wide ballots below
@@ -2237,7 +2323,7 @@ __global__ __launch_bounds__(kBlock) void sph_runs_kernel(SphLayoutArgs a, const
                              : min(64u - lane, n - t) + (other ? (uint32_t)__builtin_ctzll(other) : 64u);
   // The cell of the run's first particle, computed as the bin pass did (same state, same
   // ops), so its key is e.x; anything else (never seen) is handled as outside the grid.
-  const f4 s = st[e.y];
+  const f4 s = st[resolve_payload(e.y, nullptr, bin_prev).state];
   // The first kRunIdx particle indices (the write pass then needs no lookup gathers for
   // them), loaded together (adjacent, mostly one line).
   uint32_t idx[kRunIdx];
@@ -2314,9 +2400,10 @@ __global__ __launch_bounds__(1024) void sph_layout_scan_kernel(SphLayoutArgs a,
 constexpr uint32_t kSlotMap = 2048;
 __global__ __launch_bounds__(kBlock) void sph_layout_write_kernel(SphLayoutArgs a,
                                                                   const rps_config* __restrict__ cfg,
-                                                                  const uint2* __restrict__ lookup,
+                                                                  uint2* __restrict__ lookup,
                                                                   const f4* __restrict__ st,
                                                                   const uint32_t* __restrict__ idx_prev,
+                                                                  const uint2* __restrict__ bin_prev,
                                                                   SphSlots sl, uint32_t N, uint32_t p_slots) {
   __shared__ uint32_t lbase[kBlock], lsrc[kBlock], lidx[kRunIdx][kBlock];
   __shared__ uint8_t lcell[kSlotMap];
@@ -2362,7 +2449,7 @@ __global__ __launch_bounds__(kBlock) void sph_layout_write_kernel(SphLayoutArgs 
     }
     const uint32_t r = k - lbase[lo];
     const uint32_t i = r < kRunIdx ? lidx[r][lo] : lookup[lsrc[lo] + r].y;
-    predict_slot(cfg, st, sl, b0 + k, i, idx_prev);
+    predict_slot(cfg, st, sl, b0 + k, i, idx_prev, bin_prev);
   }
   // The listed runs' slots [part[blocks], N), spread over every thread of the launch (one slot
   // per thread at most once the launch covers N: a clump of many particles in one run costs
@@ -2377,13 +2464,15 @@ __global__ __launch_bounds__(kBlock) void sph_layout_write_kernel(SphLayoutArgs 
       else hi = mid;
     }
     const uint2 run = a.out_runs[lo];
-    predict_slot(cfg, st, sl, k, lookup[run.x + (k - run.y)].y, idx_prev);
+    predict_slot(cfg, st, sl, k, lookup[run.x + (k - run.y)].y, idx_prev, bin_prev);
   }
   // P != N: the pad slots [N, P) (never scanned) keep lookup order after the
   // layout's N storage slots; the density and sim passes compute only those that own their
-  // particle (one pushed out of [0, N) by stale entries).
+  // particle (one pushed out of [0, N) by stale entries).  These entries are the next frame's
+  // stale pads: their payloads become particle indices (kPidFlag), since the slots they name
+  // are this frame's (resolve_payload).
   for (uint32_t k = N + blockIdx.x * kBlock + threadIdx.x; k < p_slots; k += stride)
-    predict_slot(cfg, st, sl, k, lookup[k].y, idx_prev);
+    lookup[k].y = kPidFlag | predict_slot(cfg, st, sl, k, lookup[k].y, idx_prev, bin_prev);
 }
 
 // Cells owning no run take their key's storage run from run2 (complete after the write pass).
@@ -2634,6 +2723,14 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
   e = hipGetLastError();
   ++*launches;
   if (e != hipSuccess) return e;
+  // The first two later stages (one and two global passes) fold those passes into their tail
+  // launches, which then read one buffer and write the other (the neighbour masks' buffer,
+  // dead during the sort): lookup -> scratch -> lookup.  Tiles up to 4096 entries (same box,
+  // ms/frame: 50 000 0.1433 -> 0.1408, 65 536 0.0996 -> 0.0971, 10^6 0.4284 -> 0.4157; with
+  // 8192-entry tiles at 2^22 0.9239 -> 0.9255, not kept).  RPS_SPH_SORT_FOLD=0 runs them as
+  // register-fused launches.
+  const bool fold = b.sort_fold && tile_log <= 12u && stages >= first_global_stage + 2u;
+  uint2* const scratch = reinterpret_cast<uint2*>(b.sl.nbr_mask);
   for (uint32_t stage = first_global_stage; stage < stages; ++stage) {
     // Passes whose compare span 2*gw exceeds the tile are global: steps [0, T).  Up to four
     // of them run as one register-fused launch (sph_sort_fused_kernel); three or five per
@@ -2641,6 +2738,24 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
     uint32_t T = 0;
     while (T <= stage && 2u * (1u << (stage - T)) > tile) ++T;
     uint32_t step = 0;
+    if (fold && T <= 2u) {  // T == stage - first_global_stage + 1
+      uint2* dst = T == 1u ? scratch : b.lookup;
+      const uint2* src = T == 1u ? b.lookup : scratch;
+#define RPS_TAIL_FOLD(TL, NTH)                                                                          \
+  if (T == 1u) hipLaunchKernelGGL((sph_sort_tail_kernel<TL, 1>), dim3(tiles), dim3(NTH), 0, s, dst, src); \
+  else hipLaunchKernelGGL((sph_sort_tail_kernel<TL, 2>), dim3(tiles), dim3(NTH), 0, s, dst, src)
+      switch (tile_log) {
+        case 13: RPS_TAIL_FOLD(13, 1024); break;
+        case 12: RPS_TAIL_FOLD(12, 512); break;
+        case 11: RPS_TAIL_FOLD(11, 256); break;
+        default: return hipErrorInvalidValue;
+      }
+#undef RPS_TAIL_FOLD
+      e = hipGetLastError();
+      ++*launches;
+      if (e != hipSuccess) return e;
+      continue;
+    }
     // Stages with five to nine global passes run them all in one gathered-tile launch
     // (sph_sort_gather_kernel; at T = 5 and 2^22 it also beats the 32-entry register-fused
     // launch, 16.3 us: frame -4.5 us).
@@ -2676,9 +2791,9 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
     }
     if (step <= stage) {  // the stage's passes inside each tile: strides tile/2 .. 1
       switch (tile_log) {
-        case 13: hipLaunchKernelGGL((sph_sort_tail_kernel<13>), dim3(tiles), dim3(1024), 0, s, b.lookup); break;
-        case 12: hipLaunchKernelGGL((sph_sort_tail_kernel<12>), dim3(tiles), dim3(512), 0, s, b.lookup); break;
-        case 11: hipLaunchKernelGGL((sph_sort_tail_kernel<11>), dim3(tiles), dim3(256), 0, s, b.lookup); break;
+        case 13: hipLaunchKernelGGL((sph_sort_tail_kernel<13>), dim3(tiles), dim3(1024), 0, s, b.lookup, b.lookup); break;
+        case 12: hipLaunchKernelGGL((sph_sort_tail_kernel<12>), dim3(tiles), dim3(512), 0, s, b.lookup, b.lookup); break;
+        case 11: hipLaunchKernelGGL((sph_sort_tail_kernel<11>), dim3(tiles), dim3(256), 0, s, b.lookup, b.lookup); break;
         default: return hipErrorInvalidValue;  // later stages exist only with 2048..8192-entry tiles
       }
       e = hipGetLastError();
@@ -2778,7 +2893,9 @@ bool sph_layout_grid(const rps_config& c, uint32_t cell_cap, SphGrid* g) {
 
 hipError_t launch_sph_layout_pre(const SphBuffers& b, hipStream_t s) {
   const SphLayoutArgs& a = b.lay;
-  hipLaunchKernelGGL(sph_runs_kernel, dim3(blocks_for(b.n)), dim3(kBlock), 0, s, a, b.cfg, b.lookup, b.st, b.n);
+  const uint2* bin_prev = b.resident ? b.bin_next : nullptr;  // flagged pad payloads (resolve_payload)
+  hipLaunchKernelGGL(sph_runs_kernel, dim3(blocks_for(b.n)), dim3(kBlock), 0, s, a, b.cfg, b.lookup, b.st, b.n,
+                     bin_prev);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const uint32_t nparts = blocks_for(a.g.cells);
@@ -2787,7 +2904,7 @@ hipError_t launch_sph_layout_pre(const SphBuffers& b, hipStream_t s) {
   hipLaunchKernelGGL(sph_layout_scan_kernel, dim3(1), dim3(1024), 0, s, a, b.lookup, nparts);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(sph_layout_write_kernel, dim3(nparts), dim3(kBlock), 0, s, a, b.cfg, b.lookup, b.st,
-                     b.resident ? b.idx_prev : nullptr, b.sl, b.n, b.p);
+                     b.resident ? b.idx_prev : nullptr, bin_prev, b.sl, b.n, b.p);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(sph_layout_fixup_kernel, dim3(nparts), dim3(kBlock), 0, s, a, b.n);
   if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -2839,11 +2956,18 @@ hipError_t launch_sph_count(const SphBuffers& b, unsigned long long* out, hipStr
 }
 
 hipError_t launch_sph_rebin(const SphBuffers& b, const uint32_t* perm, hipStream_t s) {
-  hipLaunchKernelGGL(sph_rebin_kernel, dim3(blocks_for(b.n)), dim3(kBlock), 0, s, b.cfg, b.st, perm, b.bin_next, b.n);
+  hipLaunchKernelGGL(sph_rebin_kernel, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg, b.st, perm, b.bin_next,
+                     b.sl, b.sl.owner ? b.p : b.n);
   return hipGetLastError();
 }
-hipError_t launch_sph_materialize(const f4* st, const uint32_t* perm, f4* dst, uint32_t n, hipStream_t s) {
-  hipLaunchKernelGGL(sph_materialize_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, s, st, perm, dst, n);
+hipError_t launch_sph_materialize(const SphBuffers& b, const f4* st, const uint32_t* perm, f4* dst, hipStream_t s) {
+  const uint32_t slots = b.sl.owner ? b.p : b.n;
+  hipLaunchKernelGGL(sph_materialize_kernel, dim3(blocks_for(slots)), dim3(kBlock), 0, s, st, perm, dst, b.sl, slots);
+  return hipGetLastError();
+}
+hipError_t launch_sph_pad_unflag(const SphBuffers& b, hipStream_t s) {
+  if (b.p == b.n) return hipSuccess;
+  hipLaunchKernelGGL(sph_pad_unflag_kernel, dim3(blocks_for(b.p - b.n)), dim3(kBlock), 0, s, b.lookup, b.n, b.p);
   return hipGetLastError();
 }
 hipError_t launch_sph_lookup_translate(const uint2* lookup, const uint32_t* perm, uint2* out, uint32_t p,

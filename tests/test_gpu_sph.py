@@ -153,16 +153,17 @@ def test_sph_resident_state_frames(gpu, orc, monkeypatch, n):
                       download_at={3, 6})
 
 
-def test_sph_resident_state_api(gpu, orc, monkeypatch):
+@pytest.mark.parametrize("n", [16384, 16000])
+def test_sph_resident_state_api(gpu, orc, monkeypatch, n):
     """Every particle-order API call on slot-resident state: a device export, a partial field
     upload, a download, and gated frames (a config change resetting frame_count, SHADER_DELAY
     3) right after resident frames; the state bitwise after each step, the export bitwise
-    against the oracle's particles."""
+    against the oracle's particles.  At 16 000 (P != N) the state sits at owner slots and the
+    pad entries carry flagged particle indices between frames."""
     from hip_mem import DeviceBuffer
 
     rps = gpu
     monkeypatch.setenv("RPS_SPH_LAYOUT", "2")
-    n = 16384
     cfg = rps.default_particle_config(n, gravity=100.0)
     soa = _blob(n, 43, spread=300.0)
     st = orc.SphState(n)
@@ -364,11 +365,14 @@ def test_sph_spatial_layout_ragged(gpu, orc, monkeypatch, n):
     """The layout forced at non-power-of-two N (P = next_pow2(N) > N): the pad entries sort in
     and only [0, N) is scanned, so the layout's storage covers the N scanned
     slots in cell order and the P - N pad slots after them in lookup order; the lowest slot of
-    each particle owns it (its sim), particles pushed past N included.  Six frames bitwise."""
+    each particle owns it (its sim), particles pushed past N included.  The state stays at the
+    owner slots from frame to frame (downloads only after frames 2 and 5), the pad entries
+    carrying flagged particle indices.  Six frames bitwise."""
     rps = gpu
     monkeypatch.setenv("RPS_SPH_LAYOUT", "2")
     cfg = rps.default_particle_config(n, gravity=100.0)
-    _frames_vs_oracle(rps, orc, n, _blob(n, 90 + n, spread=max(15.0, (n ** 0.5) * 2.0)), cfg, 6)
+    _frames_vs_oracle(rps, orc, n, _blob(n, 90 + n, spread=max(15.0, (n ** 0.5) * 2.0)), cfg, 6,
+                      download_at={2})
 
 
 @pytest.mark.parametrize("layout,long_min", [("2", None), ("0", None), ("0", "8"), ("2", "128")])
@@ -401,7 +405,7 @@ def test_sph_layout_one_million(gpu, orc):
     parts = rps.setup_particles_scatter(cfg, n, seed=0x5EED)
     soa = dict(x=parts["position"][:, 0].copy(), y=parts["position"][:, 1].copy(),
                vx=parts["velocity"][:, 0].copy(), vy=parts["velocity"][:, 1].copy())
-    _frames_vs_oracle(rps, orc, n, soa, cfg, 3)
+    _frames_vs_oracle(rps, orc, n, soa, cfg, 3, download_at=set())
 
 
 @pytest.mark.parametrize("layout", ["0", "2"])

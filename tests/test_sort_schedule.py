@@ -379,3 +379,48 @@ def test_gather_stage_schedule_equals_network(T, LW, LE, kmax):
     keys = g.integers(0, kmax, P)
     a = np.stack([keys, np.arange(P)], 1).astype(np.int64)
     np.testing.assert_array_equal(gather_stage(a, s, lg, T, LW, LE), ref_passes(a, s, range(T)))
+
+
+def cas_at(va, pa, vb, pb):
+    """cas_at (rps_kernels.hip): the reference's compare-swap on entries at positions pa, pb
+    (row-wise arrays), the lower position being the left one."""
+    lo_a = pa < pb
+    lk = np.where(lo_a, va[:, 0], vb[:, 0])
+    rk = np.where(lo_a, vb[:, 0], va[:, 0])
+    sw = lk > rk
+    a, b = va[sw].copy(), vb[sw].copy()
+    va[sw], vb[sw] = b, a
+
+
+def folded_tail(a, s, TLOG, TG):
+    """sph_sort_tail_kernel<TLOG, TG>: every position's value after stage s's first TG global
+    passes, recomputed from its group (folded_global), then the tail's in-tile passes."""
+    P = len(a)
+    x = np.arange(P)
+    m = (2 << s) - 1
+    if TG == 1:
+        A, MA = a[x].copy(), a[x ^ m].copy()
+        cas_at(A, x, MA, x ^ m)
+    else:
+        h = 1 << (s - 1)
+        A, B, MA, MB = a[x].copy(), a[x ^ h].copy(), a[x ^ m].copy(), a[x ^ h ^ m].copy()
+        cas_at(A, x, MA, x ^ m)
+        cas_at(B, x ^ h, MB, x ^ h ^ m)
+        cas_at(A, x, B, x ^ h)
+        cas_at(MA, x ^ m, MB, x ^ m ^ h)
+    T = 1 << TLOG
+    return np.concatenate([tail(A[k:k + T], TLOG) for k in range(0, P, T)])
+
+
+@pytest.mark.parametrize("TLOG", [11, 13])
+@pytest.mark.parametrize("TG", [1, 2])
+@pytest.mark.parametrize("kmax", [5, 1 << 20])
+def test_folded_tail_equals_network(TLOG, TG, kmax):
+    """The folded tails of the first two later stages (s = TLOG, TLOG + 1): every pass of the
+    stage, global and in-tile, equal to the reference's, ties included, over the whole array."""
+    s = TLOG + TG - 1
+    P = 1 << (s + 2)  # two blocks of the stage's span
+    g = np.random.default_rng(TLOG * 7 + TG + (kmax & 3))
+    keys = g.integers(0, kmax, P)
+    a = np.stack([keys, np.arange(P)], 1).astype(np.int64)
+    np.testing.assert_array_equal(folded_tail(a, s, TLOG, TG), ref_passes(a, s, range(s + 1)))
