@@ -53,6 +53,8 @@ struct rps_ctx {
   uint32_t P = 0;
   uint32_t sort_passes = 0, sort_launches = 0;
   bool sort_fold = true;  // RPS_SPH_SORT_FOLD (rps_kernels.hip, launch_sph_sort)
+  bool csort = true;      // RPS_SPH_CSORT: the compact sort at 2^11 <= P <= 2^16
+  uint8_t csort_tlog = 0; // RPS_SPH_CSORT_TLOG (11..13; 0: by size)
   uint8_t sph_batch_d = 0, sph_batch_s = 0;  // forced scan batches (0: by size)
   SphLayoutArgs lay{};     // spatial record layout (RPS_SPH_LAYOUT, P >= 2^20 by default): arrays
   uint32_t cell_cap = 0;   // their cell capacity (0: no layout)
@@ -309,6 +311,8 @@ SphBuffers sph_buffers(rps_ctx* ctx) {
   b.cell_cap = ctx->cell_cap;
   b.layout = ctx->layout_last;
   b.sort_fold = ctx->sort_fold;
+  b.csort = ctx->csort;
+  b.csort_tlog = ctx->csort_tlog;
   return b;
 }
 
@@ -622,6 +626,8 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     ctx->P = next_pow2_u32((uint32_t)n);  // spatial lookup sized next_pow2 (particle_buffers.rs:86)
     const size_t P = ctx->P;
     ctx->sort_fold = env_int("RPS_SPH_SORT_FOLD", 1) != 0;
+    ctx->csort = env_int("RPS_SPH_CSORT", 1) != 0;
+    ctx->csort_tlog = (uint8_t)std::max(0, std::min(13, env_int("RPS_SPH_CSORT_TLOG", 0)));
     const int lay_mode = env_int("RPS_SPH_LAYOUT", 1);
     const bool lay_ok = lay_mode == 2 || (lay_mode == 1 && P >= (1u << 20));
     // With the layout the state is slot-resident (one entry per slot: P of them)

@@ -171,6 +171,8 @@ struct SphBuffers {
   uint8_t batch_s;   //   0: by size, sph_batch); per context, RPS_SPH_BATCH[_D|_S] at create
   bool layout;       // this frame uses the spatial record layout (lay.* valid)
   bool sort_fold;    // the first two later sort stages fold their global passes into the tails
+  bool csort;        // 2^11 <= P <= 2^16: the compact (4-byte entry) sort, RPS_SPH_CSORT
+  uint8_t csort_tlog;  // its tile (11..13; 0: by size), RPS_SPH_CSORT_TLOG
   uint32_t cell_cap; // capacity of lay.cell_info / cellrun (0: layout never available)
   SphLayoutArgs lay;
 };

@@ -1381,6 +1381,309 @@ __global__ __launch_bounds__(1u << (T + LW + 1 - LE)) __attribute__((amdgpu_wave
   lds_chunk_out<LW + KL, KL, LE>(lds, t, [&](uint32_t tau, uint2 e) { lookup[pos(tau)] = e; });
 }
 
+// ---------------------------------------------------------------------------------------
+// Compact sort (2^11 <= P <= 2^16, the reference's default N = 50 000 and C1): the same network
+// on 4-byte entries key << 16 | payload (key < N <= 2^16, payload < P <= 2^16), compared on the
+// high halves only (v_cmp_gt_u32_sdwa WORD_1), so equal keys stay in place exactly as in the
+// reference's compare-swap.  One head launch (bin + the stages inside a tile, the schedule of
+// sph_sort_head_kernel) and ONE launch per later stage: its T global passes are folded into the
+// tail launch for every T (the tiles of a stage's group each recompute the group's passes from
+// the other tiles' entries, read from one packed buffer, written to the other), so P = 2^16 is
+// five launches instead of nine.  The last launch unpacks into the uint2 lookup.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t cpack(uint2 e) { return (e.x << 16) | (e.y & 0xFFFFu); }
+__device__ __forceinline__ uint2 cunpack(uint32_t e) { return make_uint2(e >> 16, e & 0xFFFFu); }
+
+// Compare-swaps on packed entries: every compare first (the keys' high halves by SDWA), then
+// each pair's v_swap_b32 with its mask as EXEC (as cas4 on uint2 entries).
+__device__ __forceinline__ void ccas(uint32_t& a, uint32_t& b) {
+  uint64_t m, sv;
+  asm("v_cmp_gt_u32_sdwa %[m], %[a], %[b] src0_sel:WORD_1 src1_sel:WORD_1\n\t"
+      "s_mov_b64 %[sv], exec\n\t"
+      "s_mov_b64 exec, %[m]\n\t"
+      "v_swap_b32 %[a], %[b]\n\t"
+      "s_mov_b64 exec, %[sv]"
+      : [a] "+v"(a), [b] "+v"(b), [m] "=&s"(m), [sv] "=&s"(sv));
+}
+__device__ __forceinline__ void ccas2(uint32_t& a0, uint32_t& b0, uint32_t& a1, uint32_t& b1) {
+  uint64_t m0, m1, sv;
+  asm("v_cmp_gt_u32_sdwa %[m0], %[a0], %[b0] src0_sel:WORD_1 src1_sel:WORD_1\n\t"
+      "v_cmp_gt_u32_sdwa %[m1], %[a1], %[b1] src0_sel:WORD_1 src1_sel:WORD_1\n\t"
+      "s_mov_b64 %[sv], exec\n\t"
+      "s_mov_b64 exec, %[m0]\n\t"
+      "v_swap_b32 %[a0], %[b0]\n\t"
+      "s_mov_b64 exec, %[m1]\n\t"
+      "v_swap_b32 %[a1], %[b1]\n\t"
+      "s_mov_b64 exec, %[sv]"
+      : [a0] "+v"(a0), [b0] "+v"(b0), [a1] "+v"(a1), [b1] "+v"(b1), [m0] "=&s"(m0), [m1] "=&s"(m1),
+        [sv] "=&s"(sv));
+}
+__device__ __forceinline__ void ccas4(uint32_t& a0, uint32_t& b0, uint32_t& a1, uint32_t& b1, uint32_t& a2,
+                                      uint32_t& b2, uint32_t& a3, uint32_t& b3) {
+  uint64_t m0, m1, m2, m3, sv;
+  asm("v_cmp_gt_u32_sdwa %[m0], %[a0], %[b0] src0_sel:WORD_1 src1_sel:WORD_1\n\t"
+      "v_cmp_gt_u32_sdwa %[m1], %[a1], %[b1] src0_sel:WORD_1 src1_sel:WORD_1\n\t"
+      "v_cmp_gt_u32_sdwa %[m2], %[a2], %[b2] src0_sel:WORD_1 src1_sel:WORD_1\n\t"
+      "v_cmp_gt_u32_sdwa %[m3], %[a3], %[b3] src0_sel:WORD_1 src1_sel:WORD_1\n\t"
+      "s_mov_b64 %[sv], exec\n\t"
+      "s_mov_b64 exec, %[m0]\n\t"
+      "v_swap_b32 %[a0], %[b0]\n\t"
+      "s_mov_b64 exec, %[m1]\n\t"
+      "v_swap_b32 %[a1], %[b1]\n\t"
+      "s_mov_b64 exec, %[m2]\n\t"
+      "v_swap_b32 %[a2], %[b2]\n\t"
+      "s_mov_b64 exec, %[m3]\n\t"
+      "v_swap_b32 %[a3], %[b3]\n\t"
+      "s_mov_b64 exec, %[sv]"
+      : [a0] "+v"(a0), [b0] "+v"(b0), [a1] "+v"(a1), [b1] "+v"(b1), [a2] "+v"(a2), [b2] "+v"(b2),
+        [a3] "+v"(a3), [b3] "+v"(b3), [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2), [m3] "=&s"(m3),
+        [sv] "=&s"(sv));
+}
+
+// group_passes on packed entries.
+template <int K>
+__device__ __forceinline__ void cgroup_passes(uint32_t (&v)[1 << K]) {
+#pragma unroll
+  for (int m = K - 1; m >= 0; --m) {
+    if constexpr (K == 1) {
+      ccas(v[0], v[1]);
+    } else if constexpr (K == 2) {
+      const int d = 1 << m, j0 = pair_lo(0, m), j1 = pair_lo(1, m);
+      ccas2(v[j0], v[j0 + d], v[j1], v[j1 + d]);
+    } else {
+#pragma unroll
+      for (int p = 0; p < (1 << (K - 1)); p += 4) {
+        const int d = 1 << m;
+        const int j0 = pair_lo(p, m), j1 = pair_lo(p + 1, m), j2 = pair_lo(p + 2, m), j3 = pair_lo(p + 3, m);
+        ccas4(v[j0], v[j0 + d], v[j1], v[j1 + d], v[j2], v[j2 + d], v[j3], v[j3 + d]);
+      }
+    }
+  }
+}
+
+// xlane_pass on packed entries: one DPP move per entry.
+template <int CTRL, bool REV>
+__device__ __forceinline__ void cxlane_pass(uint32_t (&v)[8], bool left) {
+  uint32_t p[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) p[j] = (uint32_t)__builtin_amdgcn_mov_dpp((int)v[REV ? 7 - j : j], CTRL, 0xF, 0xF, false);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const bool swap = left ? (v[j] >> 16) > (p[j] >> 16) : (p[j] >> 16) > (v[j] >> 16);
+    v[j] = swap ? p[j] : v[j];
+  }
+}
+
+// The LDS chunks of the head and tail (lds_chunk, lds_chunks, lds_flip_chunk, lds_mid_chunks)
+// on packed entries; the same padded indices (one pad entry per 32).
+template <int LG, int K>
+__device__ __forceinline__ void clds_chunk(uint32_t* lds, uint32_t t) {
+  constexpr int LGG = LG - K + 1;
+  constexpr uint32_t g = 1u << LGG;
+  constexpr int NG = 1 << (3 - K);
+#pragma unroll
+  for (int i = 0; i < NG; ++i) {
+    const uint32_t q = chunk_group<3 - K>(t, i);
+    const uint32_t e0 = ((q >> LGG) << (LG + 1)) + (q & (g - 1u));
+    const uint32_t a = padded(e0);
+    uint32_t v[1 << K];
+#pragma unroll
+    for (int j = 0; j < (1 << K); ++j) v[j] = lds[a + pad_off<g>(j)];
+    cgroup_passes<K>(v);
+#pragma unroll
+    for (int j = 0; j < (1 << K); ++j) lds[a + pad_off<g>(j)] = v[j];
+  }
+}
+template <int LG>
+__device__ __forceinline__ void clds_chunks(uint32_t* lds, uint32_t t) {
+  if constexpr (LG >= 4) {
+    constexpr int K = LG - 3 >= 3 ? 3 : LG - 3;
+    clds_chunk<LG, K>(lds, t);
+    lds_sync<(2 << LG)>();
+    clds_chunks<LG - K>(lds, t);
+  }
+}
+template <int S>
+__device__ __forceinline__ void clds_flip_chunk(uint32_t* lds, uint32_t t) {
+  constexpr uint32_t g = 1u << (S - 1);
+  constexpr int LP = S - 2;
+  const uint32_t base = (t >> LP) << (S + 1), r = t & ((1u << LP) - 1u);
+  const uint32_t a = padded(base + r), b = padded(base + g - 1u - r);
+  uint32_t v[8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[j] = lds[a + pad_off<g>(j)];
+    v[4 + j] = lds[b + pad_off<g>(j)];
+  }
+  ccas4(v[0], v[7], v[1], v[6], v[4], v[3], v[5], v[2]);
+  ccas4(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    lds[a + pad_off<g>(j)] = v[j];
+    lds[b + pad_off<g>(j)] = v[4 + j];
+  }
+}
+template <int LG>
+__device__ __forceinline__ void clds_mid_chunks(uint32_t* lds, uint32_t t) {
+  if constexpr (LG >= 5) {
+    constexpr int K = LG - 4 >= 3 ? 3 : LG - 4;
+    clds_chunk<LG, K>(lds, t);
+    lds_sync<(2 << LG)>();
+    clds_mid_chunks<LG - K>(lds, t);
+  }
+}
+template <bool HI16>
+__device__ __forceinline__ void creg_tail(uint32_t (&v)[8], uint32_t t) {
+  if constexpr (HI16) cxlane_pass<kDppXor2, false>(v, (t & 2u) == 0u);
+  cxlane_pass<kDppXor1, false>(v, (t & 1u) == 0u);
+  cgroup_passes<3>(v);
+}
+template <int S, int TLOG>
+__device__ __forceinline__ void chead_stages(uint32_t* lds, uint32_t t, uint32_t (&v)[8]) {
+  if constexpr (S < TLOG) {
+    const uint32_t a = padded(8u * t);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) lds[a + i] = v[i];
+    lds_sync<(2 << S)>();
+    clds_flip_chunk<S>(lds, t);
+    lds_sync<(2 << S)>();
+    clds_mid_chunks<S - 2>(lds, t);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = lds[a + i];
+    creg_tail<(S >= 6)>(v, t);
+    chead_stages<S + 1, TLOG>(lds, t, v);
+  }
+}
+
+// A lane's eight consecutive entries [8t, 8t + 8) of the tile at `base`: packed (two 16-B
+// stores) or unpacked into the uint2 lookup (four).
+template <bool OUT_LOOKUP>
+__device__ __forceinline__ void cstore_eight(uint32_t* __restrict__ cout, uint2* __restrict__ lookup, uint32_t base,
+                                             uint32_t t, const uint32_t (&v)[8]) {
+  if constexpr (OUT_LOOKUP) {
+    uint4* o = reinterpret_cast<uint4*>(lookup + base + 8u * t);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint2 lo = cunpack(v[2 * i]), hi = cunpack(v[2 * i + 1]);
+      o[i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+    }
+  } else {
+    uint4* o = reinterpret_cast<uint4*>(cout + base + 8u * t);
+    o[0] = make_uint4(v[0], v[1], v[2], v[3]);
+    o[1] = make_uint4(v[4], v[5], v[6], v[7]);
+  }
+}
+
+// Bin + stages [0, TLOG) of one tile (sph_sort_head_kernel's schedule).  Entries [n, P) are the
+// previous frame's pad entries, read from the uint2 lookup (keys < N, payloads < P: both fit).
+template <int TLOG, bool OUT_LOOKUP>
+__global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_eu(4))) void sph_csort_head_kernel(
+    uint2* __restrict__ lookup, SortBin bin, uint32_t* __restrict__ cout) {
+  static_assert(TLOG >= 11 && TLOG <= 13, "eight entries per thread, 256..1024 threads");
+  constexpr uint32_t TILE = 1u << TLOG, NT = TILE / 8;
+  __shared__ uint32_t lds[TILE + TILE / 32];
+  const uint32_t t = threadIdx.x;
+  const uint32_t base0 = blockIdx.x * TILE;
+  {
+    uint2 raw[8];
+    bin_load<NT>(lookup, bin, base0, t, raw);
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) {
+      const uint32_t q = t + k * NT, gq = base0 + q;
+      const uint2 e = (gq >= bin.n || bin.prebuilt) ? raw[k] : bin_key(bin, __builtin_bit_cast(f2, raw[k]), gq);
+      lds[padded(q)] = cpack(e);
+    }
+  }
+  __syncthreads();
+  uint32_t v[8];
+  const uint32_t a = padded(8u * t);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = lds[a + i];
+  ccas4(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);  // stages 0-2 (reg_stages012)
+  ccas4(v[0], v[3], v[1], v[2], v[4], v[7], v[5], v[6]);
+  ccas4(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
+  ccas4(v[0], v[7], v[1], v[6], v[2], v[5], v[3], v[4]);
+  ccas4(v[0], v[2], v[1], v[3], v[4], v[6], v[5], v[7]);
+  ccas4(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
+  cxlane_pass<kDppXor1, true>(v, (t & 1u) == 0u);  // stage 3
+  cgroup_passes<3>(v);
+  cxlane_pass<kDppRev4, true>(v, (t & 2u) == 0u);  // stage 4
+  creg_tail<false>(v, t);
+  chead_stages<5, TLOG>(lds, t, v);
+  cstore_eight<OUT_LOOKUP>(cout, lookup, base0, t, v);
+}
+
+// The value at position x after the first TG global passes of stage s = TLOG + TG - 1 (the flip,
+// then strides 2^(s-1) .. 2^TLOG).  x's group is the 2^TG positions x ^ (a * mirror) ^ (sum of
+// b_k 2^(s-k)); indexed by u = bits [TLOG, s] of a position, the flip pairs u with ~u and the
+// later passes pair u with u ^ 2^b, the lower position (u's bit 0) being the left one: the
+// passes are a 2^TG-entry flip stage.  Held at c = u ^ ux (ux = x's u, the tile index's low bits,
+// uniform over the workgroup), x is v[0] and each pass's direction is one uniform bit of ux.
+// Only v[0] is returned, so the compiler drops the compare-swaps outside its cone.
+template <int TG>
+__device__ __forceinline__ uint32_t cfold(const uint32_t* __restrict__ src, uint32_t x, uint32_t lo) {
+  constexpr uint32_t M = 1u << TG;
+  const uint32_t s = lo + TG - 1u;
+  const uint32_t ux = (x >> lo) & (M - 1u);
+  const uint32_t lowm = (1u << lo) - 1u;
+  const uint32_t hi = x & ~((2u << s) - 1u);
+  uint32_t v[M];
+#pragma unroll
+  for (uint32_t c = 0; c < M; ++c) {
+    const uint32_t low = (c >> (TG - 1)) ? (~x & lowm) : (x & lowm);
+    v[c] = src[hi | ((ux ^ c) << lo) | low];
+  }
+  const auto pass = [&](uint32_t dim, bool flip) {
+    const bool d = (ux >> dim) & 1u;  // c's partner is the left entry
+#pragma unroll
+    for (uint32_t c = 0; c < M; ++c) {
+      if (c & (1u << dim)) continue;
+      const uint32_t c1 = flip ? (c ^ (M - 1u)) : (c | (1u << dim));
+      const uint32_t l = d ? v[c1] : v[c], r = d ? v[c] : v[c1];
+      const bool sw = (l >> 16) > (r >> 16);
+      const uint32_t nl = sw ? r : l, nr = sw ? l : r;
+      v[c] = d ? nr : nl;
+      v[c1] = d ? nl : nr;
+    }
+  };
+  pass(TG - 1u, true);
+#pragma unroll
+  for (int b = TG - 2; b >= 0; --b) pass((uint32_t)b, false);
+  return v[0];
+}
+
+// A later stage s = TLOG + TG - 1 of one tile: its TG global passes (cfold) and its in-tile passes
+// (sph_sort_tail_kernel's schedule), src -> cout, or the uint2 lookup for the last stage.
+template <int TLOG, int TG, bool OUT_LOOKUP>
+__global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_eu(4))) void sph_csort_stage_kernel(
+    const uint32_t* __restrict__ src, uint32_t* __restrict__ cout, uint2* __restrict__ lookup) {
+  static_assert(TLOG >= 11 && TLOG <= 13 && TG >= 1 && TG <= 5, "compact sort shapes");
+  constexpr uint32_t TILE = 1u << TLOG, NT = TILE / 8;
+  __shared__ uint32_t lds[TILE + TILE / 32];
+  const uint32_t t = threadIdx.x;
+  const uint32_t base0 = blockIdx.x * TILE;
+  {  // strides TILE/2, TILE/4, TILE/8 on the folded entries t + j * NT
+    uint32_t v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = cfold<TG>(src, base0 + t + j * NT, TLOG);
+    cgroup_passes<3>(v);
+    const uint32_t a = padded(t);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) lds[a + pad_off<NT>(j)] = v[j];
+  }
+  __syncthreads();
+  clds_chunks<TLOG - 4>(lds, t);
+  {  // strides 8, 4, 2, 1 (lane pair: stride 8 by DPP)
+    const uint32_t a = padded(8u * t);
+    uint32_t v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = lds[a + i];
+    cxlane_pass<kDppXor1, false>(v, (t & 1u) == 0u);
+    cgroup_passes<3>(v);
+    cstore_eight<OUT_LOOKUP>(cout, lookup, base0, t, v);
+  }
+}
+
 // calculate_spatial_lookup_offsets, compute_shader.wgsl:507-525: offsets[key] = the first
 // slot of key's run.  The same pass also records ends[key] = one past the run's last slot
 // in [0, n): the reference's scan of a run stops at the first slot whose key differs or at
@@ -2684,6 +2987,70 @@ static hipError_t launch_sort_small(uint32_t threads, hipStream_t s, uint2* look
   return hipGetLastError();
 }
 
+// Tile of the compact sort at P entries (2^11 .. 2^16): RPS_SPH_CSORT_TLOG, else by size.
+static uint32_t csort_tlog(uint32_t stages, uint32_t forced) {
+  uint32_t tl = forced ? forced : (stages <= 13u ? stages : 12u);
+  return std::max(11u, std::min(std::min(tl, 13u), stages));
+}
+
+// The compact sort (see sph_csort_head_kernel): head + one launch per later stage.
+static hipError_t launch_sph_csort(const SphBuffers& b, const SortBin& bin, uint32_t stages, hipStream_t s,
+                                   uint32_t* launches) {
+  const uint32_t P = b.p;
+  const uint32_t tl = csort_tlog(stages, b.csort_tlog);
+  const uint32_t tiles = P >> tl, nt = (1u << tl) / 8u;
+  uint32_t* const cb[2] = {reinterpret_cast<uint32_t*>(b.sl.nbr_mask),  // dead during the sort
+                           reinterpret_cast<uint32_t*>(b.sl.nbr_mask) + P};
+  const bool one = stages == tl;
+#define RPS_CHEAD(TL)                                                                                         \
+  if (one) hipLaunchKernelGGL((sph_csort_head_kernel<TL, true>), dim3(tiles), dim3(nt), 0, s, b.lookup, bin, cb[0]); \
+  else hipLaunchKernelGGL((sph_csort_head_kernel<TL, false>), dim3(tiles), dim3(nt), 0, s, b.lookup, bin, cb[0])
+  switch (tl) {
+    case 11: RPS_CHEAD(11); break;
+    case 12: RPS_CHEAD(12); break;
+    default: RPS_CHEAD(13); break;
+  }
+#undef RPS_CHEAD
+  hipError_t e = hipGetLastError();
+  ++*launches;
+  if (e != hipSuccess) return e;
+  for (uint32_t stage = tl, k = 0; stage < stages; ++stage, ++k) {
+    const uint32_t tg = stage - tl + 1u;
+    const bool last = stage + 1u == stages;
+    const uint32_t* src = cb[k & 1u];
+    uint32_t* dst = cb[(k + 1u) & 1u];
+#define RPS_CSTAGE(TL, TG)                                                                                        \
+  case TG:                                                                                                        \
+    if (last) hipLaunchKernelGGL((sph_csort_stage_kernel<TL, TG, true>), dim3(tiles), dim3(nt), 0, s, src, dst, b.lookup); \
+    else hipLaunchKernelGGL((sph_csort_stage_kernel<TL, TG, false>), dim3(tiles), dim3(nt), 0, s, src, dst, b.lookup); \
+    break
+    switch (tl) {
+      case 11:
+        switch (tg) { RPS_CSTAGE(11, 1); RPS_CSTAGE(11, 2); RPS_CSTAGE(11, 3); RPS_CSTAGE(11, 4); RPS_CSTAGE(11, 5);
+          default: return hipErrorInvalidValue; }
+        break;
+      case 12:
+        switch (tg) { RPS_CSTAGE(12, 1); RPS_CSTAGE(12, 2); RPS_CSTAGE(12, 3); RPS_CSTAGE(12, 4);
+          default: return hipErrorInvalidValue; }
+        break;
+      default:
+        switch (tg) { RPS_CSTAGE(13, 1); RPS_CSTAGE(13, 2); RPS_CSTAGE(13, 3);
+          default: return hipErrorInvalidValue; }
+    }
+#undef RPS_CSTAGE
+    e = hipGetLastError();
+    ++*launches;
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+// Whether this frame's sort runs compact: 2^11 <= P <= 2^16 and every lookup payload below 2^16
+// (pad entries of a layout frame with P != N carry kPidFlag).
+static bool csort_ok(const SphBuffers& b) {
+  return b.csort && b.p >= 2048u && b.p <= 65536u && (b.p == b.n || b.cell_cap == 0u);
+}
+
 // Passes 1-2 of the frame: bin (folded into the first sort launch) + the bitonic network.
 hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
                            uint32_t* launches) {
@@ -2694,6 +3061,7 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
   *launches = 0;
   // Slot-resident state: the previous layout frame's sim wrote the bin entries (key, slot).
   const SortBin bin{b.cfg, b.st, b.offsets, b.n, b.lay.run2, b.resident ? b.bin_next : nullptr};
+  if (csort_ok(b)) return launch_sph_csort(b, bin, stages, s, launches);
   if (stages == 0) {  // P == 1: nothing to sort, only bin
     hipLaunchKernelGGL((sph_sort_local_kernel<true, 1>), dim3(1), dim3(64), 0, s, b.lookup, 1u, 1u, 0u,
                        0u, bin, 0u);

@@ -424,3 +424,65 @@ def test_folded_tail_equals_network(TLOG, TG, kmax):
     keys = g.integers(0, kmax, P)
     a = np.stack([keys, np.arange(P)], 1).astype(np.int64)
     np.testing.assert_array_equal(folded_tail(a, s, TLOG, TG), ref_passes(a, s, range(s + 1)))
+
+
+def cfold(a, x, lo, TG):
+    """cfold<TG> (rps_kernels.hip): the value at each position x after the first TG global passes
+    of stage s = lo + TG - 1, computed as the kernel does: the group held at c = u ^ ux (u = bits
+    [lo, s] of a position, ux = x's), each pass's direction one bit of ux, x = v[0]."""
+    M = 1 << TG
+    s = lo + TG - 1
+    ux = (x >> lo) & (M - 1)
+    lowm = (1 << lo) - 1
+    hi = x & ~((2 << s) - 1)
+    v = []
+    for c in range(M):
+        low = np.where(c >> (TG - 1), ~x & lowm, x & lowm)
+        v.append(a[hi | ((ux ^ c) << lo) | low].copy())
+
+    def pas(dim, flip):
+        d = ((ux >> dim) & 1) == 1  # c's partner is the left entry
+        for c in range(M):
+            if c & (1 << dim):
+                continue
+            c1 = c ^ (M - 1) if flip else c | (1 << dim)
+            l = np.where(d[:, None], v[c1], v[c])
+            r = np.where(d[:, None], v[c], v[c1])
+            sw = l[:, 0] > r[:, 0]
+            nl = np.where(sw[:, None], r, l)
+            nr = np.where(sw[:, None], l, r)
+            v[c] = np.where(d[:, None], nr, nl)
+            v[c1] = np.where(d[:, None], nl, nr)
+
+    pas(TG - 1, True)
+    for b in range(TG - 2, -1, -1):
+        pas(b, False)
+    return v[0]
+
+
+@pytest.mark.parametrize("TLOG,TG", [(11, 1), (11, 2), (11, 3), (11, 4), (11, 5), (12, 4), (13, 3)])
+@pytest.mark.parametrize("kmax", [5, 1 << 16])
+def test_compact_stage_equals_network(TLOG, TG, kmax):
+    """sph_csort_stage_kernel<TLOG, TG>: every later stage of the compact sort (P <= 2^16) folds all
+    its TG global passes (cfold) in front of the tail's in-tile passes; equal to the reference's
+    passes of stage s = TLOG + TG - 1 over the whole array, ties included."""
+    s = TLOG + TG - 1
+    P = 1 << (s + 1) if TG >= 4 else 1 << (s + 2)  # whole blocks of the stage's span
+    g = np.random.default_rng(TLOG * 5 + TG * 3 + (kmax & 7))
+    keys = g.integers(0, kmax, P)
+    a = np.stack([keys, np.arange(P)], 1).astype(np.int64)
+    folded = cfold(a, np.arange(P), TLOG, TG)
+    T = 1 << TLOG
+    out = np.concatenate([tail(folded[k:k + T], TLOG) for k in range(0, P, T)])
+    np.testing.assert_array_equal(out, ref_passes(a, s, range(s + 1)))
+
+
+def test_compact_entries_fit():
+    """The compact sort's packing: key << 16 | payload with key < N <= P <= 2^16 and payload < P;
+    comparing the high halves orders by key alone (equal keys compare equal, whatever the
+    payloads), as the reference's key compare (wgsl:494-503)."""
+    g = np.random.default_rng(3)
+    k = g.integers(0, 1 << 16, (1000, 2)).astype(np.uint32)
+    p = g.integers(0, 1 << 16, (1000, 2)).astype(np.uint32)
+    packed = (k << np.uint32(16)) | p
+    np.testing.assert_array_equal((packed[:, 0] >> 16) > (packed[:, 1] >> 16), k[:, 0] > k[:, 1])

@@ -21,6 +21,9 @@ for step in "$@"; do
     tests)
       run pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf --durations=15 --timeout 300 --timeout-method thread; rc=$?
       [ $rc -le 1 ] || exit $rc ;;
+    tests_sph)
+      run pytest_gpu_sph 600 python -u -m pytest tests/test_gpu_sph.py tests/test_gpu_golden.py -m gpu -q -rf -x --timeout 120 --timeout-method thread; rc=$?
+      [ $rc -le 1 ] || exit $rc ;;
     smoke)
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench)
@@ -39,6 +42,11 @@ for step in "$@"; do
     prof_sph:*)
       n=${step#prof_sph:}
       run prof_sph_$n 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_sph_$n -o run --output-format csv -- python3 tools/sph_frames.py $n 60 || exit $? ;;
+    pmc_sph:*)
+      # pmc_sph:N:C1,C2,...  one rocprofv3 --pmc pass (counters of one pass only) over SPH frames
+      spec=${step#pmc_sph:}; n=${spec%%:*}; cs=${spec#*:}
+      tag=$(echo "$cs" | tr ',' '\n' | head -1)
+      run pmc_sph_${n}_$tag 120 rocprofv3 --kernel-trace --pmc ${cs//,/ } -d gpurun_out/pmc_sph_${n}_$tag -o run --output-format csv -- python3 tools/sph_frames.py $n 30 || exit $? ;;
     prof_sph64k)
       run prof_sph64k 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_sph64k -o run --output-format csv -- python3 tools/sph_frames.py 65536 60 || exit $? ;;
     probe)
