@@ -55,6 +55,7 @@ struct rps_ctx {
   bool sort_fold = true;  // RPS_SPH_SORT_FOLD (rps_kernels.hip, launch_sph_sort)
   bool csort = true;      // RPS_SPH_CSORT: the compact sort at 2^11 <= P <= 2^16
   uint8_t csort_tlog = 0; // RPS_SPH_CSORT_TLOG (11..13; 0: by size)
+  uint32_t pair_max_p = 0; // RPS_SPH_PAIRS: lane-pair scans up to this P
   uint8_t sph_batch_d = 0, sph_batch_s = 0;  // forced scan batches (0: by size)
   SphLayoutArgs lay{};     // spatial record layout (RPS_SPH_LAYOUT, P >= 2^20 by default): arrays
   uint32_t cell_cap = 0;   // their cell capacity (0: no layout)
@@ -70,6 +71,7 @@ struct rps_ctx {
   uint2* bin_next = nullptr;
   bool resident = false;
   bool keys_valid = false;      // bin_next matches st and the current config
+  bool pkeys_valid = false;     // bin_next = (key, i) of the particle-order state (no layout)
   const uint32_t* lookup_perm = nullptr;  // the lookup's payloads are slots of this perm
   // N-body
   f2* pos_all = nullptr;
@@ -297,6 +299,7 @@ SphBuffers sph_buffers(rps_ctx* ctx) {
   b.bin_next = ctx->bin_next;
   b.idx_prev = ctx->idx_alt;  // during a resident frame: the perm its sort payloads refer to
   b.resident = ctx->resident;
+  b.pkeys = ctx->pkeys_valid;
   b.sl = ctx->sl;
   b.ends = ctx->ends;
   b.lookup = ctx->lookup;
@@ -313,6 +316,7 @@ SphBuffers sph_buffers(rps_ctx* ctx) {
   b.sort_fold = ctx->sort_fold;
   b.csort = ctx->csort;
   b.csort_tlog = ctx->csort_tlog;
+  b.pair_max_p = ctx->pair_max_p;
   return b;
 }
 
@@ -474,6 +478,7 @@ int sph_canonical(rps_ctx* ctx) {
   set_sph_fields(ctx);
   ctx->resident = false;
   ctx->keys_valid = false;
+  ctx->pkeys_valid = false;
   return RPS_OK;
 }
 
@@ -513,6 +518,7 @@ int step_sph_sim(rps_ctx* ctx, bool layout, const SphGrid& g) {
     ctx->resident = true;
     ctx->keys_valid = true;
   }
+  ctx->pkeys_valid = !layout;  // else the sim wrote (key, i) for the next frame
   return RPS_OK;
 }
 
@@ -628,6 +634,7 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     ctx->sort_fold = env_int("RPS_SPH_SORT_FOLD", 1) != 0;
     ctx->csort = env_int("RPS_SPH_CSORT", 1) != 0;
     ctx->csort_tlog = (uint8_t)std::max(0, std::min(13, env_int("RPS_SPH_CSORT_TLOG", 0)));
+    ctx->pair_max_p = (uint32_t)std::max(0, env_int("RPS_SPH_PAIRS", 1 << 17));
     const int lay_mode = env_int("RPS_SPH_LAYOUT", 1);
     const bool lay_ok = lay_mode == 2 || (lay_mode == 1 && P >= (1u << 20));
     // With the layout the state is slot-resident (one entry per slot: P of them)
@@ -678,8 +685,9 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
       // sim's bin entries
       slots.push_back({(void**)&ctx->st_alt, align_up(st_n * sizeof(f4), 256)});
       slots.push_back({(void**)&ctx->idx_alt, align_up(P * sizeof(uint32_t), 256)});
-      slots.push_back({(void**)&ctx->bin_next, align_up(n * sizeof(uint2), 256)});
     }
+    // the sim's bin entries for the next frame (slot-resident or particle order)
+    slots.push_back({(void**)&ctx->bin_next, align_up(n * sizeof(uint2), 256)});
   }
   if (ctx->mode == RPS_MODE_NBODY) {
     ctx->ns_padded = (global + kNbodyTile - 1) / kNbodyTile * kNbodyTile;
@@ -782,6 +790,7 @@ int rps_set_config(rps_ctx* ctx, const rps_config* cfg, const rps_ext_config* ex
   ctx->ext = e;
   ctx->have_config = true;
   ctx->keys_valid = false;  // slot-resident bin entries were keyed with the old config
+  ctx->pkeys_valid = false;
   // write_buffer(config) (src/particle_buffers.rs:230-236): the 144 B ride in a one-wave
   // kernel's arguments, ordered on the context stream before the next step's kernels.  A
   // pinned-staging hipMemcpyAsync cost 12-18 us a frame at 65 536 particles (STREAM) and
@@ -805,6 +814,7 @@ int rps_upload_particles(rps_ctx* ctx, const rps_particle* aos, uint64_t offset,
   const uint64_t chunk = std::min<uint64_t>(n, kStagingChunk);
   if (n == 0) return RPS_OK;
   if ((rc = sph_canonical(ctx))) return rc;
+  ctx->pkeys_valid = false;  // the state changes
   rc = ensure_staging(ctx, chunk);
   if (rc) return rc;
   for (uint64_t done = 0; done < n; done += chunk) {
@@ -874,6 +884,7 @@ int rps_upload_field(rps_ctx* ctx, int field, const float* src, uint64_t offset,
   if (offset + n > ctx->n) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "range exceeds particle_count");
   if (n == 0) return RPS_OK;
   if ((rc = sph_canonical(ctx))) return rc;
+  ctx->pkeys_valid = false;  // the state changes
   if (!life) p = field_ptr(ctx, field);  // (sph_canonical may have swapped the state buffer)
   if (!life && ctx->layout.mask == plain_layout().mask) {
     RPS_HIP(ctx, hipMemcpyAsync(p + offset, src, n * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
@@ -1016,6 +1027,7 @@ int rps_init_scatter(rps_ctx* ctx, uint64_t seed) {
   a.key1 = (uint32_t)(seed >> 32);
   ctx->resident = false;  // every particle rewritten in particle order
   ctx->keys_valid = false;
+  ctx->pkeys_valid = false;
   RPS_HIP(ctx, launch_init_scatter(a, ctx->stream));
   if (ctx->next)
     RPS_HIP(ctx, launch_next_rebuild(ctx->exp, ctx->next, 0, ctx->n, ctx->n, (uint32_t)ctx->life_clock,

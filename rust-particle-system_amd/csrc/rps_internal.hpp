@@ -165,6 +165,9 @@ struct SphBuffers {
   uint2* bin_next;   // N
   const uint32_t* idx_prev;  // N (resident only)
   bool resident;
+  // Without the layout, the last active frame's sim wrote bin_next[i] = (key, i) from the state
+  // and config the next frame bins (rps_context.hip tracks their validity): its sort head reads them.
+  bool pkeys;
   uint32_t n;        // N
   uint32_t p;        // next_pow2(N)
   uint8_t batch_d;   // scan entries in flight per lane, density / sim pass (4, 8, 16;
@@ -173,6 +176,7 @@ struct SphBuffers {
   bool sort_fold;    // the first two later sort stages fold their global passes into the tails
   bool csort;        // 2^11 <= P <= 2^16: the compact (4-byte entry) sort, RPS_SPH_CSORT
   uint8_t csort_tlog;  // its tile (11..13; 0: by size), RPS_SPH_CSORT_TLOG
+  uint32_t pair_max_p;  // P <= this: density / sim scans by lane pairs (RPS_SPH_PAIRS)
   uint32_t cell_cap; // capacity of lay.cell_info / cellrun (0: layout never available)
   SphLayoutArgs lay;
 };

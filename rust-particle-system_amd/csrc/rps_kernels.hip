@@ -661,14 +661,18 @@ struct SortBin {
   uint32_t n;
   uint2* run2;  // spatial layout's storage runs, reset with offsets (nullptr: no layout)
   const uint2* prebuilt;  // bin entries the previous frame's sim wrote (nullptr: from positions)
+  bool reset_pre;         // prebuilt entries in particle order (no layout): still reset offsets/run2
 };
 
 __device__ __forceinline__ f2 bin_pos(const SortBin& b, uint32_t i) {
   return reinterpret_cast<const f2*>(b.st)[2u * i];
 }
-__device__ __forceinline__ uint2 bin_key(const SortBin& b, f2 pos, uint32_t i) {
+__device__ __forceinline__ void bin_reset(const SortBin& b, uint32_t i) {
   b.offsets[i] = 0xFFFFFFFFu;
   if (b.run2) b.run2[i] = make_uint2(0xFFFFFFFFu, 0u);
+}
+__device__ __forceinline__ uint2 bin_key(const SortBin& b, f2 pos, uint32_t i) {
+  bin_reset(b, i);
   if (b.prebuilt) return b.prebuilt[i];  // slot-resident state: (key, slot), keyed by the sim
   const float r = b.cfg->smoothing_radius;
   const int32_t cx = f32_to_i32((pos[0] + b.cfg->screen_bounds[1]) / r);
@@ -1249,7 +1253,8 @@ __device__ __forceinline__ void bin_keys(const SortBin& bin, uint32_t base0, uin
     if (gq >= bin.n) {
       s[q] = raw[k];
     } else if (bin.prebuilt) {  // (key, slot) of a layout frame: run2 is reset by the runs kernel,
-      s[q] = raw[k];             // offsets on debug readback (rps_read_debug)
+      if (bin.reset_pre) bin_reset(bin, gq);  // offsets on debug readback (rps_read_debug); the
+      s[q] = raw[k];                           // sim's (key, i) of a frame without layout: both
     } else {
       s[q] = bin_key(bin, __builtin_bit_cast(f2, raw[k]), gq);
     }
@@ -1590,6 +1595,7 @@ __global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_e
 #pragma unroll
     for (uint32_t k = 0; k < 8; ++k) {
       const uint32_t q = t + k * NT, gq = base0 + q;
+      if (gq < bin.n && bin.prebuilt && bin.reset_pre) bin_reset(bin, gq);
       const uint2 e = (gq >= bin.n || bin.prebuilt) ? raw[k] : bin_key(bin, __builtin_bit_cast(f2, raw[k]), gq);
       lds[padded(q)] = cpack(e);
     }
@@ -1613,46 +1619,61 @@ __global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_e
   cstore_eight<OUT_LOOKUP>(cout, lookup, base0, t, v);
 }
 
-// The value at position x after the first TG global passes of stage s = TLOG + TG - 1 (the flip,
-// then strides 2^(s-1) .. 2^TLOG).  x's group is the 2^TG positions x ^ (a * mirror) ^ (sum of
-// b_k 2^(s-k)); indexed by u = bits [TLOG, s] of a position, the flip pairs u with ~u and the
-// later passes pair u with u ^ 2^b, the lower position (u's bit 0) being the left one: the
-// passes are a 2^TG-entry flip stage.  Held at c = u ^ ux (ux = x's u, the tile index's low bits,
-// uniform over the workgroup), x is v[0] and each pass's direction is one uniform bit of ux.
-// Only v[0] is returned, so the compiler drops the compare-swaps outside its cone.
+// The values at positions x0 .. x0 + 3 (x0 = 0 mod 4) after the first TG global passes of stage
+// s = TLOG + TG - 1 (the flip, then strides 2^(s-1) .. 2^TLOG).  A position x's group is the 2^TG
+// positions x ^ (a * mirror) ^ (sum of b_k 2^(s-k)); indexed by u = bits [TLOG, s] of a position,
+// the flip pairs u with ~u and the later passes pair u with u ^ 2^b, the lower position (u's bit
+// 0) being the left one: the passes are a 2^TG-entry flip stage.  Held at c = u ^ ux (ux = x's u,
+// the tile index's low bits, uniform over the workgroup), x is v[0], and each pass's direction is
+// one uniform bit of ux (a scalar branch per pass).  The four positions' groups are four
+// consecutive entries of each tile of the group (reversed in the mirrored ones): one 16-B load
+// per tile.  Only v[0] is kept, so the compiler drops the compare-swaps outside its cone.
+__device__ __forceinline__ void cas_keep(uint32_t& l, uint32_t& r) {
+  const bool sw = (l >> 16) > (r >> 16);
+  const uint32_t nl = sw ? r : l, nr = sw ? l : r;
+  l = nl;
+  r = nr;
+}
 template <int TG>
-__device__ __forceinline__ uint32_t cfold(const uint32_t* __restrict__ src, uint32_t x, uint32_t lo) {
+__device__ __forceinline__ uint4 cfold4(const uint32_t* __restrict__ src, uint32_t x0, uint32_t lo) {
   constexpr uint32_t M = 1u << TG;
   const uint32_t s = lo + TG - 1u;
-  const uint32_t ux = (x >> lo) & (M - 1u);
+  const uint32_t ux = (x0 >> lo) & (M - 1u);
   const uint32_t lowm = (1u << lo) - 1u;
-  const uint32_t hi = x & ~((2u << s) - 1u);
-  uint32_t v[M];
+  const uint32_t hi = x0 & ~((2u << s) - 1u);
+  uint32_t v[4][M];
 #pragma unroll
   for (uint32_t c = 0; c < M; ++c) {
-    const uint32_t low = (c >> (TG - 1)) ? (~x & lowm) : (x & lowm);
-    v[c] = src[hi | ((ux ^ c) << lo) | low];
+    const bool mir = c >> (TG - 1);
+    const uint32_t low = mir ? (lowm - 3u - (x0 & lowm)) : (x0 & lowm);
+    const uint4 w = *reinterpret_cast<const uint4*>(src + (hi | ((ux ^ c) << lo) | low));
+    v[0][c] = mir ? w.w : w.x;
+    v[1][c] = mir ? w.z : w.y;
+    v[2][c] = mir ? w.y : w.z;
+    v[3][c] = mir ? w.x : w.w;
   }
   const auto pass = [&](uint32_t dim, bool flip) {
-    const bool d = (ux >> dim) & 1u;  // c's partner is the left entry
 #pragma unroll
     for (uint32_t c = 0; c < M; ++c) {
       if (c & (1u << dim)) continue;
       const uint32_t c1 = flip ? (c ^ (M - 1u)) : (c | (1u << dim));
-      const uint32_t l = d ? v[c1] : v[c], r = d ? v[c] : v[c1];
-      const bool sw = (l >> 16) > (r >> 16);
-      const uint32_t nl = sw ? r : l, nr = sw ? l : r;
-      v[c] = d ? nr : nl;
-      v[c1] = d ? nl : nr;
+      if ((ux >> dim) & 1u) {  // c's partner is the left entry
+#pragma unroll
+        for (int i = 0; i < 4; ++i) cas_keep(v[i][c1], v[i][c]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) cas_keep(v[i][c], v[i][c1]);
+      }
     }
   };
   pass(TG - 1u, true);
 #pragma unroll
   for (int b = TG - 2; b >= 0; --b) pass((uint32_t)b, false);
-  return v[0];
+  return make_uint4(v[0][0], v[1][0], v[2][0], v[3][0]);
 }
 
-// A later stage s = TLOG + TG - 1 of one tile: its TG global passes (cfold) and its in-tile passes
+// A later stage s = TLOG + TG - 1 of one tile: its TG global passes (cfold4, four consecutive
+// positions per thread and 16-B loads, through LDS to the tail's order) and its in-tile passes
 // (sph_sort_tail_kernel's schedule), src -> cout, or the uint2 lookup for the last stage.
 template <int TLOG, int TG, bool OUT_LOOKUP>
 __global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_eu(4))) void sph_csort_stage_kernel(
@@ -1662,16 +1683,26 @@ __global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_e
   __shared__ uint32_t lds[TILE + TILE / 32];
   const uint32_t t = threadIdx.x;
   const uint32_t base0 = blockIdx.x * TILE;
-  {  // strides TILE/2, TILE/4, TILE/8 on the folded entries t + j * NT
+#pragma unroll
+  for (uint32_t k = 0; k < 2; ++k) {  // the folded entries 4 (t + k NT) .. + 3
+    const uint32_t q = 4u * (t + k * NT);
+    const uint4 f = cfold4<TG>(src, base0 + q, TLOG);
+    lds[padded(q)] = f.x;  // q = 0 mod 4: the four share one pad offset
+    lds[padded(q) + 1u] = f.y;
+    lds[padded(q) + 2u] = f.z;
+    lds[padded(q) + 3u] = f.w;
+  }
+  __syncthreads();
+  {  // strides TILE/2, TILE/4, TILE/8 on the entries t + j * NT
+    const uint32_t a = padded(t);
     uint32_t v[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = cfold<TG>(src, base0 + t + j * NT, TLOG);
+    for (int j = 0; j < 8; ++j) v[j] = lds[a + pad_off<NT>(j)];
     cgroup_passes<3>(v);
-    const uint32_t a = padded(t);
 #pragma unroll
     for (int j = 0; j < 8; ++j) lds[a + pad_off<NT>(j)] = v[j];
   }
-  __syncthreads();
+  lds_sync<TILE>();
   clds_chunks<TLOG - 4>(lds, t);
   {  // strides 8, 4, 2, 1 (lane pair: stride 8 by DPP)
     const uint32_t a = padded(8u * t);
@@ -2087,6 +2118,80 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
   density_store(cfg, sl, t, p_slots, p, d, nd, m0, m1);
 }
 
+// Lane pairs (small P: one slot per lane leaves a single wave per SIMD, and each wave waits on
+// one lane's chain of gathers).  Lanes 2k and 2k + 1 take the same slot: the even lane gathers
+// and evaluates flat entries f, f + 2, ..., the odd lane f + 1, f + 3, ...; each lane then takes
+// its partner's terms by DPP and BOTH add every entry in the reference's order (entry f + 2u,
+// then f + 2u + 1), so the pair holds identical sums, masks and loop conditions: the same
+// additions in the same order as one lane, twice the waves and half the chain per lane.
+__device__ __forceinline__ float pair_f(float v) {  // the partner lane's value (lane ^ 1)
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), kDppXor1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ uint32_t pair_u(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kDppXor1, 0xF, 0xF, false);
+}
+
+// calculate_density (wgsl:207-254) by lane pairs; otherwise sph_density_kernel.
+template <int kScanBatch, bool LAYOUT>
+__global__ __launch_bounds__(kBlock) void sph_density2_kernel(const rps_config* __restrict__ cfg,
+                                                              RunBounds rb, SphSlots sl, uint32_t p_slots) {
+  const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t t = g >> 1, par = g & 1u;
+  if (t >= p_slots) return;  // pair-uniform, as every condition below
+  const uint32_t N = cfg->particle_count;
+  if (LAYOUT && par == 0u && t <= N / 32u) rb.keybits[t] = 0u;
+  if (sl.owner && t >= N && !owner_is(sl, sl.idx_s[t], t)) return;
+  const f2 p = sl.pp_s[t];
+  const float r = cfg->smoothing_radius, r2 = r * r;
+  const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
+  __shared__ RunTable runs;
+  const uint32_t total = nine_runs<LAYOUT>(rb, p[0], p[1], cfg->screen_bounds[1],
+                                   cfg->screen_bounds[3], r, N, runs);
+  RunCursor rc(runs);
+  float d = 0.0f, nd = 0.0f;
+  uint64_t m0 = 0, m1 = 0;
+  const bool own_finite = fabsf(p[0]) < INFINITY && fabsf(p[1]) < INFINITY;
+  if (sl.longq) {
+    const bool defer = long_scan(sl, total, p);
+    wave_append(defer && par == 0u, sl.longq_n, sl.longq,
+                make_uint4(t + 1u, __float_as_uint(p[0]), __float_as_uint(p[1]), 0u));
+    if (defer) return;
+  }
+  const bool may_stop = own_finite || total > 128u;
+  for (uint32_t f = 0; f < total && !(may_stop && d != d && nd != nd); f += 2u * kScanBatch) {
+    f2 q[kScanBatch];
+#pragma unroll
+    for (int u = 0; u < kScanBatch; ++u) q[u] = sl.pp_s[rc.slot_skip(min(f + 2u * u + par, total - 1u))];
+#pragma unroll
+    for (int u = 0; u < kScanBatch; ++u) {
+      const uint32_t b = f + 2u * u + par;  // this lane's entry
+      const float dx = p[0] - q[u][0], dy = p[1] - q[u][1];
+      const float sq = dx * dx + dy * dy;
+      const bool in = b < total && !(sq > r2);
+      f2 k = f2{0.0f, 0.0f};
+      if (in) k = density_terms(sq, r, dn, ndn);
+      const float k0o = pair_f(k[0]), k1o = pair_f(k[1]);
+      const bool ino = pair_u(in ? 1u : 0u) != 0u;
+      const bool ie = par ? ino : in, io = par ? in : ino;  // entries f + 2u (even), f + 2u + 1
+      if (ie) {
+        d = d + (par ? k0o : k[0]);
+        nd = nd + (par ? k1o : k[1]);
+      }
+      if (io) {
+        d = d + (par ? k[0] : k0o);
+        nd = nd + (par ? k[1] : k1o);
+      }
+      if (total <= 128u) {
+        const uint32_t be = f + 2u * u;
+        const uint64_t bits = (ie ? 1ull : 0ull) | (io ? 2ull : 0ull);
+        if (be < 64u) m0 |= bits << be;  // be is even: both bits in one word
+        else m1 |= bits << (be - 64u);
+      }
+    }
+  }
+  if (par == 0u) density_store(cfg, sl, t, p_slots, p, d, nd, m0, m1);
+}
+
 // A long scan of the density pass (kLongScan): one queued slot per wave, 64 entries per step.
 template <bool LAYOUT>
 __global__ __launch_bounds__(kBlock) void sph_density_long_kernel(const rps_config* __restrict__ cfg,
@@ -2268,6 +2373,12 @@ __device__ __forceinline__ void sim_finish(const rps_config* __restrict__ cfg, c
     bin_next[i] = make_uint2(cell_key(cx, cy, cfg->particle_count), t);
   } else {
     st[i] = f4{ox, oy, qx, qy};
+    if (bin_next) {  // the next frame's bin entry in particle order (SphBuffers::pkeys)
+      const float r = cfg->smoothing_radius;
+      const int32_t cx = f32_to_i32((ox + cfg->screen_bounds[1]) / r);
+      const int32_t cy = f32_to_i32((oy + cfg->screen_bounds[3]) / r);
+      bin_next[i] = make_uint2(cell_key(cx, cy, cfg->particle_count), i);
+    }
   }
 }
 
@@ -2332,6 +2443,162 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
   else
     scan_runs<kScanBatch, kPads>(sl, runs, 0u, total, p, r2, self, load_pv, viscosity, viscosity_nan);
   sim_finish<LAYOUT>(cfg, sl, st, bin_next, t, o.i, qx, qy, wx, wy);
+}
+
+// Lane-pair drivers of the sim's scans (see sph_density2_kernel): the entries split between the
+// lanes of a pair -- masked: the set bits alternately (the even lane the 1st, 3rd, ... of each
+// batch's pairs of bits); runs: flat entries f + 2u + par --, each lane evaluating its entries'
+// terms (term(q), for entries within the radius that are not the particle itself), and both
+// lanes adding every entry's terms in the reference's order through add(terms, use, par).
+__device__ __forceinline__ bool pop_bit(uint64_t& m0, uint64_t& m1, uint32_t& f) {
+  if (m0) {
+    f = (uint32_t)__builtin_ctzll(m0);
+    m0 &= m0 - 1u;
+    return true;
+  }
+  if (m1) {
+    f = 64u + (uint32_t)__builtin_ctzll(m1);
+    m1 &= m1 - 1u;
+    return true;
+  }
+  return false;
+}
+template <int kScanBatch, bool kPads, class T, class Load, class Term, class Add, class Done>
+__device__ __forceinline__ void scan_masked2(const SphSlots& sl, const RunTable& runs, uint64_t m0, uint64_t m1,
+                                             uint32_t self, uint32_t par, Load&& load, Term&& term, Add&& add,
+                                             Done&& done) {
+  RunCursor rc(runs);
+  uint32_t prev = 0u;
+  while ((m0 | m1) && !done()) {
+    uint32_t fs[kScanBatch], qi[kScanBatch];
+    bool live[kScanBatch];
+    f4 q[kScanBatch];
+#pragma unroll
+    for (int u = 0; u < kScanBatch; ++u) {  // the next two set bits, lowest first: even, odd
+      uint32_t fe = 0u, fo = 0u;
+      const bool le = pop_bit(m0, m1, fe);
+      const bool lo = pop_bit(m0, m1, fo);
+      live[u] = par ? lo : le;
+      // an idle lane re-reads an entry it may read (the loop runs while the even lane has one)
+      fs[u] = live[u] ? (par ? fo : fe) : (le ? fe : prev);
+      prev = fs[u];
+    }
+#pragma unroll
+    for (int u = 0; u < kScanBatch; ++u) {
+      const uint32_t j = rc.slot_skip(fs[u]);
+      q[u] = load(j);
+      qi[u] = kPads ? sl.idx_s[j] : j;
+    }
+#pragma unroll
+    for (int u = 0; u < kScanBatch; ++u) {
+      const bool use = live[u] && qi[u] != self;
+      T w{};
+      if (use) w = term(q[u]);
+      add(w, use, par);
+    }
+  }
+}
+template <int kScanBatch, bool kPads, class T, class Load, class Term, class Add, class Done>
+__device__ __forceinline__ void scan_runs2(const SphSlots& sl, const RunTable& runs, uint32_t total, f2 p, float r2,
+                                           uint32_t self, uint32_t par, Load&& load, Term&& term, Add&& add,
+                                           Done&& done) {
+  RunCursor rc(runs);
+  for (uint32_t f = 0; f < total && !done(); f += 2u * kScanBatch) {
+    f4 q[kScanBatch];
+    uint32_t qi[kScanBatch];
+#pragma unroll
+    for (int u = 0; u < kScanBatch; ++u) {
+      const uint32_t j = rc.slot_skip(min(f + 2u * u + par, total - 1u));
+      q[u] = load(j);
+      qi[u] = kPads ? sl.idx_s[j] : j;
+    }
+#pragma unroll
+    for (int u = 0; u < kScanBatch; ++u) {
+      const float dx = q[u][0] - p[0], dy = q[u][1] - p[1];
+      const bool use = f + 2u * u + par < total && qi[u] != self && !(dx * dx + dy * dy > r2);
+      T w{};
+      if (use) w = term(q[u]);
+      add(w, use, par);
+    }
+  }
+}
+
+// simulation_step (wgsl:435-453) by lane pairs; otherwise sph_sim_kernel.
+template <int kScanBatch, bool kPads, bool LAYOUT>
+__global__ __launch_bounds__(kBlock) void sph_sim2_kernel(const rps_config* __restrict__ cfg,
+                                                          RunBounds rb, SphSlots sl, f4* __restrict__ st,
+                                                          uint2* __restrict__ bin_next, uint32_t p_slots) {
+  const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t t = g >> 1, par = g & 1u;
+  if (t >= p_slots) return;
+  const SimOwn o = sim_own(cfg, sl, t);
+  if (kPads && !owner_is(sl, o.i, t)) return;
+  const uint32_t self = kPads ? o.i : t;
+  const float dt = cfg->fixed_delta_time;
+  const float r = cfg->smoothing_radius, r2 = r * r;
+  const uint32_t N = cfg->particle_count;
+  const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
+  const float vn = cfg->viscocity_kernel_norm;
+  const f2 p = o.p;
+  __shared__ RunTable runs;
+  const uint32_t total = nine_runs<LAYOUT>(rb, p[0], p[1], cfg->screen_bounds[1],
+                                   cfg->screen_bounds[3], r, N, runs);
+  const bool masked = total <= 128u;
+  if (sl.longq && long_scan(sl, total, p)) return;
+  const uint64_t m0 = masked ? sl.nbr_mask[t] : 0u, m1 = masked ? sl.nbr_mask[p_slots + t] : 0u;
+  float fx = 0.0f, fy = 0.0f;
+  const auto load_pd = [&](uint32_t j) { return sl.rec_pd[j]; };
+  const auto pterm = [&](const f4& q) { return pressure_terms(q, p, o.P_rho2, o.Pn_rho2, r, dn, ndn); };
+  const auto padd = [&](const f4& w, bool use, uint32_t pr) {
+    const f4 wo = f4{pair_f(w[0]), pair_f(w[1]), pair_f(w[2]), pair_f(w[3])};
+    const bool uo = pair_u(use ? 1u : 0u) != 0u;
+    const f4 we = pr ? wo : w, wd = pr ? w : wo;  // entries of the even lane, then the odd
+    if (pr ? uo : use) {
+      fx = fx + we[0];
+      fy = fy + we[1];
+      fx = fx + we[2];
+      fy = fy + we[3];
+    }
+    if (pr ? use : uo) {
+      fx = fx + wd[0];
+      fy = fy + wd[1];
+      fx = fx + wd[2];
+      fy = fy + wd[3];
+    }
+  };
+  const auto pressure_nan = [&] { return fx != fx && fy != fy; };
+  if (masked)
+    scan_masked2<kScanBatch, kPads, f4>(sl, runs, m0, m1, self, par, load_pd, pterm, padd, pressure_nan);
+  else
+    scan_runs2<kScanBatch, kPads, f4>(sl, runs, total, p, r2, self, par, load_pd, pterm, padd, pressure_nan);
+  const f4 own_pv = sl.rec_pv[t];
+  const float qx = own_pv[2] + fx * dt;
+  const float qy = own_pv[3] + fy * dt;
+  float wx = 0.0f, wy = 0.0f;
+  const auto load_pv = [&](uint32_t j) { return sl.rec_pv[j]; };
+  const auto vterm = [&](const f4& q) {
+    const float k = viscosity_weight(q, p, r, vn);
+    return f2{(q[2] - qx) * k, (q[3] - qy) * k};
+  };
+  const auto vadd = [&](const f2& w, bool use, uint32_t pr) {
+    const f2 wo = f2{pair_f(w[0]), pair_f(w[1])};
+    const bool uo = pair_u(use ? 1u : 0u) != 0u;
+    const f2 we = pr ? wo : w, wd = pr ? w : wo;
+    if (pr ? uo : use) {
+      wx = wx + we[0];
+      wy = wy + we[1];
+    }
+    if (pr ? use : uo) {
+      wx = wx + wd[0];
+      wy = wy + wd[1];
+    }
+  };
+  const auto viscosity_nan = [&] { return wx != wx && wy != wy; };
+  if (masked)
+    scan_masked2<kScanBatch, kPads, f2>(sl, runs, m0, m1, self, par, load_pv, vterm, vadd, viscosity_nan);
+  else
+    scan_runs2<kScanBatch, kPads, f2>(sl, runs, total, p, r2, self, par, load_pv, vterm, vadd, viscosity_nan);
+  if (par == 0u) sim_finish<LAYOUT>(cfg, sl, st, bin_next, t, o.i, qx, qy, wx, wy);
 }
 
 // The sim pass of the density pass's queued slots (kLongScan), one per wave: lane l evaluates
@@ -3060,7 +3327,10 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
   *passes = stages * (stages + 1u) / 2u;
   *launches = 0;
   // Slot-resident state: the previous layout frame's sim wrote the bin entries (key, slot).
-  const SortBin bin{b.cfg, b.st, b.offsets, b.n, b.lay.run2, b.resident ? b.bin_next : nullptr};
+  // Without the layout, the previous active frame's sim wrote (key, i) for the current state and
+  // config (SphBuffers::pkeys): the head reads them instead of keying the positions.
+  const SortBin bin{b.cfg, b.st, b.offsets, b.n, b.lay.run2,
+                    b.resident || b.pkeys ? b.bin_next : nullptr, !b.resident && b.pkeys};
   if (csort_ok(b)) return launch_sph_csort(b, bin, stages, s, launches);
   if (stages == 0) {  // P == 1: nothing to sort, only bin
     hipLaunchKernelGGL((sph_sort_local_kernel<true, 1>), dim3(1), dim3(64), 0, s, b.lookup, 1u, 1u, 0u,
@@ -3203,6 +3473,20 @@ static uint32_t long_blocks(uint32_t p) { return std::min<uint32_t>(blocks_for(p
 
 static hipError_t launch_sph_density(const SphBuffers& b, hipStream_t s) {
   const RunBounds rb = run_bounds(b);
+  if (b.p <= b.pair_max_p) {  // lane pairs (sph_density2_kernel)
+#define RPS_DENSITY2(B)                                                                              \
+  if (b.layout)                                                                                      \
+    hipLaunchKernelGGL((sph_density2_kernel<B, true>), dim3(blocks_for(2u * b.p)), dim3(kBlock), 0, s, \
+                       b.cfg, rb, b.sl, b.p);                                                         \
+  else                                                                                               \
+    hipLaunchKernelGGL((sph_density2_kernel<B, false>), dim3(blocks_for(2u * b.p)), dim3(kBlock), 0, s, \
+                       b.cfg, rb, b.sl, b.p)
+    switch (b.batch_d) {
+      case 8: RPS_DENSITY2(8); break;
+      default: RPS_DENSITY2(4); break;
+    }
+#undef RPS_DENSITY2
+  } else {
 #define RPS_DENSITY(B)                                                                            \
   if (b.layout)                                                                                   \
     hipLaunchKernelGGL((sph_density_kernel<B, true>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s, \
@@ -3210,12 +3494,13 @@ static hipError_t launch_sph_density(const SphBuffers& b, hipStream_t s) {
   else                                                                                            \
     hipLaunchKernelGGL((sph_density_kernel<B, false>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s, \
                        b.cfg, rb, b.sl, b.p)
-  switch (sph_batch(true, b.p, b.batch_d, b.layout)) {
-    case 4: RPS_DENSITY(4); break;
-    case 16: RPS_DENSITY(16); break;
-    default: RPS_DENSITY(8); break;
-  }
+    switch (sph_batch(true, b.p, b.batch_d, b.layout)) {
+      case 4: RPS_DENSITY(4); break;
+      case 16: RPS_DENSITY(16); break;
+      default: RPS_DENSITY(8); break;
+    }
 #undef RPS_DENSITY
+  }
   if (b.sl.longq) {
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -3294,11 +3579,31 @@ hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s) {
   else                                                                                              \
     hipLaunchKernelGGL((sph_sim_kernel<B, true, false>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s, \
                        b.cfg, rb, b.sl, b.st, b.bin_next, b.p)
-  switch (sph_batch(false, b.p, b.batch_s, b.layout)) {
-    case 4: RPS_SIM(4); break;
-    case 6: RPS_SIM(6); break;
-    case 16: RPS_SIM(16); break;
-    default: RPS_SIM(8); break;
+  if (b.p <= b.pair_max_p) {  // lane pairs (sph_sim2_kernel)
+#define RPS_SIM2(B)                                                                                          \
+  {                                                                                                          \
+    const dim3 g2(blocks_for(2u * b.p));                                                                     \
+    if (b.layout && b.p == b.n)                                                                              \
+      hipLaunchKernelGGL((sph_sim2_kernel<B, false, true>), g2, dim3(kBlock), 0, s, b.cfg, rb, b.sl, b.st, b.bin_next, b.p); \
+    else if (b.layout)                                                                                       \
+      hipLaunchKernelGGL((sph_sim2_kernel<B, true, true>), g2, dim3(kBlock), 0, s, b.cfg, rb, b.sl, b.st, b.bin_next, b.p);  \
+    else if (b.p == b.n)                                                                                     \
+      hipLaunchKernelGGL((sph_sim2_kernel<B, false, false>), g2, dim3(kBlock), 0, s, b.cfg, rb, b.sl, b.st, b.bin_next, b.p); \
+    else                                                                                                     \
+      hipLaunchKernelGGL((sph_sim2_kernel<B, true, false>), g2, dim3(kBlock), 0, s, b.cfg, rb, b.sl, b.st, b.bin_next, b.p); \
+  }
+    switch (b.batch_s) {
+      case 4: RPS_SIM2(4); break;
+      default: RPS_SIM2(2); break;
+    }
+#undef RPS_SIM2
+  } else {
+    switch (sph_batch(false, b.p, b.batch_s, b.layout)) {
+      case 4: RPS_SIM(4); break;
+      case 6: RPS_SIM(6); break;
+      case 16: RPS_SIM(16); break;
+      default: RPS_SIM(8); break;
+    }
   }
 #undef RPS_SIM
   if (b.sl.longq) {
