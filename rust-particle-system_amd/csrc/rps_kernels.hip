@@ -1904,7 +1904,8 @@ struct RunBounds {
 
 template <bool LAYOUT>
 __device__ __forceinline__ uint32_t nine_runs(const RunBounds& rb, float px, float py, float xoff,
-                                              float yoff, float r, uint32_t N, RunTable& runs) {
+                                              float yoff, float r, uint32_t N, RunTable& runs,
+                                              uint32_t* nruns = nullptr) {
   const int32_t cx = f32_to_i32((px + xoff) / r);  // particle_position_to_cell_coord, wgsl:121-130
   const int32_t cy = f32_to_i32((py + yoff) / r);
   uint32_t s[9], e[9];
@@ -1959,7 +1960,38 @@ __device__ __forceinline__ uint32_t nine_runs(const RunBounds& rb, float px, flo
     }
   }
   if (m) runs[m - 1u][threadIdx.x] = last;
+  if (nruns) *nruns = m;
   return c;
+}
+
+// The run table in registers (the long scans: every lane looks up entries of one slot's list at
+// once, with no chain of LDS reads): slot(f) = f + x of the last run whose start is <= f.
+struct RunRegs {
+  uint2 r[9];
+  uint32_t n;
+  __device__ RunRegs(const RunTable& t, uint32_t nr) : n(nr) {
+#pragma unroll
+    for (int m = 0; m < 9; ++m) r[m] = t[m][threadIdx.x];
+  }
+  __device__ __forceinline__ uint32_t slot(uint32_t f) const {
+    uint32_t x = r[0].x;
+#pragma unroll
+    for (uint32_t m = 1; m < 9; ++m)
+      if (m < n && f >= r[m - 1].y) x = r[m].x;
+    return f + x;
+  }
+};
+
+// The in-order sum of a long scan (one wave, one slot): the lanes' terms of the entries that
+// count, compacted in entry order into the wave's LDS buffer, then read back by every lane
+// (broadcast reads, eight in flight) and added one entry after another -- the particle's own
+// order, as v_readlane per entry did at several times the cost.
+template <class T>
+__device__ __forceinline__ uint32_t long_compact(T* buf, uint32_t base, bool in, const T& w) {
+  const uint64_t m = __builtin_amdgcn_ballot_w64(in);
+  const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  if (in) buf[base + below] = w;
+  return base + (uint32_t)__builtin_popcountll(m);
 }
 
 // Walks the flat index forward: slot(f) for non-decreasing f < total.
@@ -1994,10 +2026,6 @@ struct RunCursor {
 constexpr uint32_t kLongSub = 4;  // entries per lane in flight in the long-scan kernels (256 per wave)
 __device__ __forceinline__ bool long_scan(const SphSlots& sl, uint32_t total, f2 p) {
   return total > sl.long_min && fabsf(p[0]) < INFINITY && fabsf(p[1]) < INFINITY;
-}
-
-__device__ __forceinline__ float readlane_f(float v, uint32_t lane) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)lane));
 }
 
 // Appends v for every lane with `want` to q (one atomic per wave).
@@ -2196,37 +2224,49 @@ __global__ __launch_bounds__(kBlock) void sph_density2_kernel(const rps_config* 
 template <bool LAYOUT>
 __global__ __launch_bounds__(kBlock) void sph_density_long_kernel(const rps_config* __restrict__ cfg,
                                                                   RunBounds rb, SphSlots sl, uint32_t p_slots) {
-  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t nw = gridDim.x * (kBlock / 64u);
   const uint32_t N = cfg->particle_count;
   const float r = cfg->smoothing_radius, r2 = r * r;
   const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
   __shared__ RunTable runs;
-  for (uint32_t k = blockIdx.x * (kBlock / 64u) + (threadIdx.x >> 6);; k += nw) {
+  __shared__ f2 terms[kBlock / 64u][64u * kLongSub];
+  for (uint32_t k = blockIdx.x * (kBlock / 64u) + wv;; k += nw) {
     const uint4 e = sl.longq[k];
     if (!e.x) break;  // past the last entry
     const uint32_t t = e.x - 1u;
     const f2 p = f2{__uint_as_float(e.y), __uint_as_float(e.z)};
-    // Every lane builds the slot's table in its own column: lane l then walks entries l, l + 64, ...
-    const uint32_t total = nine_runs<LAYOUT>(rb, p[0], p[1], cfg->screen_bounds[1], cfg->screen_bounds[3], r, N, runs);
-    RunCursor rc(runs);
+    // Every lane builds the slot's table in its own column and holds it in registers: lane l then
+    // looks up entries l, l + 64, ... directly.
+    uint32_t nr = 0;
+    const uint32_t total = nine_runs<LAYOUT>(rb, p[0], p[1], cfg->screen_bounds[1], cfg->screen_bounds[3], r, N, runs, &nr);
+    const RunRegs rr(runs, nr);
     float d = 0.0f, nd = 0.0f;
     for (uint32_t f0 = 0; f0 < total; f0 += 64u * kLongSub) {
       f2 q[kLongSub];
 #pragma unroll
-      for (uint32_t u = 0; u < kLongSub; ++u) q[u] = sl.pp_s[rc.slot_skip(min(f0 + 64u * u + lane, total - 1u))];
+      for (uint32_t u = 0; u < kLongSub; ++u) q[u] = sl.pp_s[rr.slot(min(f0 + 64u * u + lane, total - 1u))];
+      uint32_t cnt = 0;
 #pragma unroll
       for (uint32_t u = 0; u < kLongSub; ++u) {
-        const uint32_t f = f0 + 64u * u + lane;
         const float dx = p[0] - q[u][0], dy = p[1] - q[u][1];
         const float sq = dx * dx + dy * dy;
         const f2 kk = density_terms(sq, r, dn, ndn);
-        for (uint64_t m = __builtin_amdgcn_ballot_w64(f < total && !(sq > r2)); m; m &= m - 1u) {
-          const uint32_t b = (uint32_t)__builtin_ctzll(m);  // entries in increasing f: the lane's order
-          d = d + readlane_f(kk[0], b);
-          nd = nd + readlane_f(kk[1], b);
-        }
+        cnt = long_compact(terms[wv], cnt, f0 + 64u * u + lane < total && !(sq > r2), kk);
       }
+      wave_lds_sync();
+      for (uint32_t i = 0; i < cnt; i += 8u) {  // entries in increasing f: the lane's order
+        f2 w[8];
+#pragma unroll
+        for (uint32_t j = 0; j < 8u; ++j) w[j] = terms[wv][min(i + j, cnt - 1u)];
+#pragma unroll
+        for (uint32_t j = 0; j < 8u; ++j)
+          if (i + j < cnt) {
+            d = d + w[j][0];
+            nd = nd + w[j][1];
+          }
+      }
+      wave_lds_sync();  // the next chunk rewrites the buffer
       if (d != d && nd != nd) break;  // NaN whatever follows (more than 128 entries: no mask)
     }
     if (lane == 0u) density_store(cfg, sl, t, p_slots, p, d, nd, 0ull, 0ull);
@@ -2602,12 +2642,13 @@ __global__ __launch_bounds__(kBlock) void sph_sim2_kernel(const rps_config* __re
 }
 
 // The sim pass of the density pass's queued slots (kLongScan), one per wave: lane l evaluates
-// flat entries l, l + 64, ... of both scans; the sums add the lanes' terms entry by entry.
+// flat entries l, l + 64, ... of both scans; the sums add the lanes' terms entry by entry
+// (long_compact, then every lane reads them back in order).
 template <bool kPads, bool LAYOUT>
 __global__ __launch_bounds__(kBlock) void sph_sim_long_kernel(const rps_config* __restrict__ cfg,
                                                               RunBounds rb, SphSlots sl, f4* __restrict__ st,
                                                               uint2* __restrict__ bin_next) {
-  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t nw = gridDim.x * (kBlock / 64u);
   const float dt = cfg->fixed_delta_time;
   const float r = cfg->smoothing_radius, r2 = r * r;
@@ -2616,13 +2657,18 @@ __global__ __launch_bounds__(kBlock) void sph_sim_long_kernel(const rps_config* 
   const float vn = cfg->viscocity_kernel_norm;
   if (blockIdx.x == 0u && threadIdx.x == 0u) *sl.longq_n = 0u;  // the density pass's appends are done
   __shared__ RunTable runs;
-  for (uint32_t k = blockIdx.x * (kBlock / 64u) + (threadIdx.x >> 6);; k += nw) {
+  __shared__ f4 terms[kBlock / 64u][64u * kLongSub];
+  f4* const tb = terms[wv];
+  f2* const tv = reinterpret_cast<f2*>(terms[wv]);
+  for (uint32_t k = blockIdx.x * (kBlock / 64u) + wv;; k += nw) {
     const uint4 e = sl.longq[k];
     if (!e.x) break;  // past the last entry
     if (lane == 0u) sl.longq[k].x = 0u;  // cleared for the next active frame
     const uint32_t t = e.x - 1u;
     const f2 p = f2{__uint_as_float(e.y), __uint_as_float(e.z)};
-    const uint32_t total = nine_runs<LAYOUT>(rb, p[0], p[1], cfg->screen_bounds[1], cfg->screen_bounds[3], r, N, runs);
+    uint32_t nr = 0;
+    const uint32_t total = nine_runs<LAYOUT>(rb, p[0], p[1], cfg->screen_bounds[1], cfg->screen_bounds[3], r, N, runs, &nr);
+    const RunRegs rr(runs, nr);
     const SimOwn o = sim_own(cfg, sl, t);
     const f4 own_pv = sl.rec_pv[t];
     if (kPads && !owner_is(sl, o.i, t)) continue;  // a repeat (wave-uniform)
@@ -2632,11 +2678,11 @@ __global__ __launch_bounds__(kBlock) void sph_sim_long_kernel(const rps_config* 
     // gathered together; the viscosity terms need the pressure sums, so a list longer than one
     // chunk gathers its velocity records again after the pressure scan.
     const bool one = total <= 64u * kLongSub;
-    const auto gather = [&](RunCursor& rc, uint32_t f0, const f4* rec, f4 (&q)[kLongSub], f4 (&qv)[kLongSub],
+    const auto gather = [&](uint32_t f0, const f4* rec, f4 (&q)[kLongSub], f4 (&qv)[kLongSub],
                             bool (&in)[kLongSub], bool both) {
       uint32_t j[kLongSub], qi[kLongSub];
 #pragma unroll
-      for (uint32_t u = 0; u < kLongSub; ++u) j[u] = rc.slot_skip(min(f0 + 64u * u + lane, total - 1u));
+      for (uint32_t u = 0; u < kLongSub; ++u) j[u] = rr.slot(min(f0 + 64u * u + lane, total - 1u));
 #pragma unroll
       for (uint32_t u = 0; u < kLongSub; ++u) {
         q[u] = rec[j[u]];
@@ -2652,47 +2698,60 @@ __global__ __launch_bounds__(kBlock) void sph_sim_long_kernel(const rps_config* 
     f4 qv[kLongSub];
     bool in1[kLongSub];
     float fx = 0.0f, fy = 0.0f;
-    {
-      RunCursor rc(runs);
-      for (uint32_t f0 = 0; f0 < total && !(fx != fx && fy != fy); f0 += 64u * kLongSub) {
-        f4 q[kLongSub];
-        gather(rc, f0, sl.rec_pd, q, qv, in1, one);
+    for (uint32_t f0 = 0; f0 < total && !(fx != fx && fy != fy); f0 += 64u * kLongSub) {
+      f4 q[kLongSub];
+      gather(f0, sl.rec_pd, q, qv, in1, one);
+      uint32_t cnt = 0;
 #pragma unroll
-        for (uint32_t u = 0; u < kLongSub; ++u) {
-          const f4 w = pressure_terms(q[u], p, o.P_rho2, o.Pn_rho2, r, dn, ndn);
-          for (uint64_t m = __builtin_amdgcn_ballot_w64(in1[u]); m; m &= m - 1u) {
-            const uint32_t b = (uint32_t)__builtin_ctzll(m);
-            fx = fx + readlane_f(w[0], b);
-            fy = fy + readlane_f(w[1], b);
-            fx = fx + readlane_f(w[2], b);
-            fy = fy + readlane_f(w[3], b);
+      for (uint32_t u = 0; u < kLongSub; ++u)
+        cnt = long_compact(tb, cnt, in1[u], pressure_terms(q[u], p, o.P_rho2, o.Pn_rho2, r, dn, ndn));
+      wave_lds_sync();
+      for (uint32_t i = 0; i < cnt; i += 8u) {
+        f4 w[8];
+#pragma unroll
+        for (uint32_t j = 0; j < 8u; ++j) w[j] = tb[min(i + j, cnt - 1u)];
+#pragma unroll
+        for (uint32_t j = 0; j < 8u; ++j)
+          if (i + j < cnt) {
+            fx = fx + w[j][0];
+            fy = fy + w[j][1];
+            fx = fx + w[j][2];
+            fy = fy + w[j][3];
           }
-        }
       }
+      wave_lds_sync();
     }
     const float qx = own_pv[2] + fx * dt;
     const float qy = own_pv[3] + fy * dt;
     float wx = 0.0f, wy = 0.0f;
     const auto visc = [&](const f4 (&q)[kLongSub], const bool (&in)[kLongSub]) {
+      uint32_t cnt = 0;
 #pragma unroll
       for (uint32_t u = 0; u < kLongSub; ++u) {
         const float kw = viscosity_weight(q[u], p, r, vn);
-        const float tx = (q[u][2] - qx) * kw, ty = (q[u][3] - qy) * kw;
-        for (uint64_t m = __builtin_amdgcn_ballot_w64(in[u]); m; m &= m - 1u) {
-          const uint32_t b = (uint32_t)__builtin_ctzll(m);
-          wx = wx + readlane_f(tx, b);
-          wy = wy + readlane_f(ty, b);
-        }
+        cnt = long_compact(tv, cnt, in[u], f2{(q[u][2] - qx) * kw, (q[u][3] - qy) * kw});
       }
+      wave_lds_sync();
+      for (uint32_t i = 0; i < cnt; i += 8u) {
+        f2 w[8];
+#pragma unroll
+        for (uint32_t j = 0; j < 8u; ++j) w[j] = tv[min(i + j, cnt - 1u)];
+#pragma unroll
+        for (uint32_t j = 0; j < 8u; ++j)
+          if (i + j < cnt) {
+            wx = wx + w[j][0];
+            wy = wy + w[j][1];
+          }
+      }
+      wave_lds_sync();
     };
     if (one) {
       visc(qv, in1);  // rec_pv's position is rec_pd's: the same entries pass the test
     } else {
-      RunCursor rc(runs);
       for (uint32_t f0 = 0; f0 < total && !(wx != wx && wy != wy); f0 += 64u * kLongSub) {
         f4 q[kLongSub];
         bool in[kLongSub];
-        gather(rc, f0, sl.rec_pv, q, qv, in, false);
+        gather(f0, sl.rec_pv, q, qv, in, false);
         visc(q, in);
       }
     }
