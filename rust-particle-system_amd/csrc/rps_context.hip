@@ -654,6 +654,7 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     if (P != n && env_int("RPS_SPH_LONGQ", 1) != 0) {
       slots.push_back({(void**)&ctx->sl.longq, align_up((P + 1) * sizeof(uint4), 256)});
       slots.push_back({(void**)&ctx->sl.longq_n, 256});
+      slots.push_back({(void**)&ctx->sl.longtab, align_up((P + 1) * kLongTab * sizeof(uint2), 256)});
       // More than 64 entries up to P = 2^19 (same box, ms/frame: 50 000 0.1523 -> 0.1406,
       // 100 000 0.1797 -> 0.1665, 300 000 and 20 000 unchanged; 48 at 50 000: 0.2822), more than
       // 128 above (10^6: 0.4423 with 128, 0.4519 with 64).

@@ -104,6 +104,7 @@ hipError_t launch_nbody_integrate(const NbodyIntegrateArgs& a, hipStream_t s);
 constexpr uint32_t kPidFlag = 0x80000000u;
 // Scans of more entries than this are "long" (rps_kernels.hip): the masks' capacity.
 constexpr uint32_t kLongScan = 128u;
+constexpr uint32_t kLongTab = 10u;  // uint2 per queued slot in SphSlots::longtab
 struct SphSlots {
   f2* pp_s;      // P predicted positions                    (density scan: 8 B/entry)
   f4* rec_pv;    // P {predicted x, y, post-gravity vx, vy}  (viscosity scan)
@@ -126,6 +127,7 @@ struct SphSlots {
   // sim's long kernel zeroes for the next active frame.
   uint4* longq;
   uint32_t* longq_n;
+  uint2* longtab;     // per queue entry: the slot's nine-run table (9 x {slot - f, f end}) + {runs, total}
   uint32_t long_min;  // a scan of more entries than this is long (kLongScan; RPS_SPH_LONG_MIN)
 };
 // Cell range of the spatial record layout (rps_kernels.hip): cells [cx_lo, cx_lo + w) x

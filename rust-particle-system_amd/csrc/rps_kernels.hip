@@ -1973,6 +1973,11 @@ struct RunRegs {
 #pragma unroll
     for (int m = 0; m < 9; ++m) r[m] = t[m][threadIdx.x];
   }
+  __device__ explicit RunRegs(const uint2* g) {  // a long_table_store record (total in r9.y)
+#pragma unroll
+    for (int m = 0; m < 9; ++m) r[m] = g[m];
+    n = g[9].x;
+  }
   __device__ __forceinline__ uint32_t slot(uint32_t f) const {
     uint32_t x = r[0].x;
 #pragma unroll
@@ -2029,9 +2034,9 @@ __device__ __forceinline__ bool long_scan(const SphSlots& sl, uint32_t total, f2
 }
 
 // Appends v for every lane with `want` to q (one atomic per wave).
-__device__ __forceinline__ void wave_append(bool want, uint32_t* count, uint4* q, uint4 v) {
+__device__ __forceinline__ uint32_t wave_append(bool want, uint32_t* count, uint4* q, uint4 v) {
   const uint64_t m = __builtin_amdgcn_ballot_w64(want);
-  if (!m) return;
+  if (!m) return 0u;
   const uint32_t leader = (uint32_t)__builtin_ctzll(m);
   const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
   uint32_t base = 0u;
@@ -2039,6 +2044,19 @@ __device__ __forceinline__ void wave_append(bool want, uint32_t* count, uint4* q
   base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)leader);
   const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
   if (want) q[base + below] = v;
+  return base + below;  // this lane's entry (when it appended)
+}
+
+// A queued slot's run table for the long kernels (the density pass has it in LDS): entries 0-8
+// the table, entry 9 {runs, total}; the long kernels load it with the queue entry, in place of
+// the keys and the 18 offsets/ends (or cellrun) loads and the table build.
+__device__ __forceinline__ void long_table_store(const SphSlots& sl, uint32_t k, const RunTable& runs,
+                                                 uint32_t nr, uint32_t total) {
+  uint2* o = sl.longtab + (size_t)k * kLongTab;
+#pragma unroll
+  for (uint32_t m = 0; m < 9u; ++m)
+    if (m < nr) o[m] = runs[m][threadIdx.x];
+  o[9] = make_uint2(nr, total);
 }
 
 // Work mapping of the density and sim passes: thread t takes lookup slot t of all P.  Lanes
@@ -2100,8 +2118,9 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
   const float r = cfg->smoothing_radius, r2 = r * r;
   const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
   __shared__ RunTable runs;
+  uint32_t nr = 0;
   const uint32_t total = nine_runs<LAYOUT>(rb, p[0], p[1], cfg->screen_bounds[1],
-                                   cfg->screen_bounds[3], r, N, runs);
+                                   cfg->screen_bounds[3], r, N, runs, &nr);
   RunCursor rc(runs);
   float d = 0.0f, nd = 0.0f;
   uint64_t m0 = 0, m1 = 0;
@@ -2117,8 +2136,12 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
   const bool own_finite = fabsf(p[0]) < INFINITY && fabsf(p[1]) < INFINITY;
   if (sl.longq) {  // long scans go to sph_density_long_kernel (see there)
     const bool defer = long_scan(sl, total, p);
-    wave_append(defer, sl.longq_n, sl.longq, make_uint4(t + 1u, __float_as_uint(p[0]), __float_as_uint(p[1]), 0u));
-    if (defer) return;
+    const uint32_t k =
+        wave_append(defer, sl.longq_n, sl.longq, make_uint4(t + 1u, __float_as_uint(p[0]), __float_as_uint(p[1]), 0u));
+    if (defer) {
+      long_table_store(sl, k, runs, nr, total);
+      return;
+    }
   }
   const bool may_stop = own_finite || total > 128u;
   for (uint32_t f = 0; f < total && !(may_stop && d != d && nd != nd); f += kScanBatch) {
@@ -2173,17 +2196,21 @@ __global__ __launch_bounds__(kBlock) void sph_density2_kernel(const rps_config* 
   const float r = cfg->smoothing_radius, r2 = r * r;
   const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
   __shared__ RunTable runs;
+  uint32_t nr = 0;
   const uint32_t total = nine_runs<LAYOUT>(rb, p[0], p[1], cfg->screen_bounds[1],
-                                   cfg->screen_bounds[3], r, N, runs);
+                                   cfg->screen_bounds[3], r, N, runs, &nr);
   RunCursor rc(runs);
   float d = 0.0f, nd = 0.0f;
   uint64_t m0 = 0, m1 = 0;
   const bool own_finite = fabsf(p[0]) < INFINITY && fabsf(p[1]) < INFINITY;
   if (sl.longq) {
     const bool defer = long_scan(sl, total, p);
-    wave_append(defer && par == 0u, sl.longq_n, sl.longq,
-                make_uint4(t + 1u, __float_as_uint(p[0]), __float_as_uint(p[1]), 0u));
-    if (defer) return;
+    const uint32_t k = wave_append(defer && par == 0u, sl.longq_n, sl.longq,
+                                   make_uint4(t + 1u, __float_as_uint(p[0]), __float_as_uint(p[1]), 0u));
+    if (defer) {
+      if (par == 0u) long_table_store(sl, k, runs, nr, total);
+      return;
+    }
   }
   const bool may_stop = own_finite || total > 128u;
   for (uint32_t f = 0; f < total && !(may_stop && d != d && nd != nd); f += 2u * kScanBatch) {
@@ -2226,21 +2253,19 @@ __global__ __launch_bounds__(kBlock) void sph_density_long_kernel(const rps_conf
                                                                   RunBounds rb, SphSlots sl, uint32_t p_slots) {
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t nw = gridDim.x * (kBlock / 64u);
-  const uint32_t N = cfg->particle_count;
   const float r = cfg->smoothing_radius, r2 = r * r;
   const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
-  __shared__ RunTable runs;
   __shared__ f2 terms[kBlock / 64u][64u * kLongSub];
   for (uint32_t k = blockIdx.x * (kBlock / 64u) + wv;; k += nw) {
     const uint4 e = sl.longq[k];
     if (!e.x) break;  // past the last entry
     const uint32_t t = e.x - 1u;
     const f2 p = f2{__uint_as_float(e.y), __uint_as_float(e.z)};
-    // Every lane builds the slot's table in its own column and holds it in registers: lane l then
-    // looks up entries l, l + 64, ... directly.
-    uint32_t nr = 0;
-    const uint32_t total = nine_runs<LAYOUT>(rb, p[0], p[1], cfg->screen_bounds[1], cfg->screen_bounds[3], r, N, runs, &nr);
-    const RunRegs rr(runs, nr);
+    // The slot's run table as the density pass stored it, in registers: lane l looks up entries
+    // l, l + 64, ... directly.
+    const uint2* tg = sl.longtab + (size_t)k * kLongTab;
+    const RunRegs rr(tg);
+    const uint32_t total = tg[9].y;
     float d = 0.0f, nd = 0.0f;
     for (uint32_t f0 = 0; f0 < total; f0 += 64u * kLongSub) {
       f2 q[kLongSub];
@@ -2255,7 +2280,8 @@ __global__ __launch_bounds__(kBlock) void sph_density_long_kernel(const rps_conf
         cnt = long_compact(terms[wv], cnt, f0 + 64u * u + lane < total && !(sq > r2), kk);
       }
       wave_lds_sync();
-      for (uint32_t i = 0; i < cnt; i += 8u) {  // entries in increasing f: the lane's order
+      // entries in increasing f: the lane's order; a sum NaN in both components stays NaN
+      for (uint32_t i = 0; i < cnt && !(d != d && nd != nd); i += 8u) {
         f2 w[8];
 #pragma unroll
         for (uint32_t j = 0; j < 8u; ++j) w[j] = terms[wv][min(i + j, cnt - 1u)];
@@ -2652,11 +2678,9 @@ __global__ __launch_bounds__(kBlock) void sph_sim_long_kernel(const rps_config* 
   const uint32_t nw = gridDim.x * (kBlock / 64u);
   const float dt = cfg->fixed_delta_time;
   const float r = cfg->smoothing_radius, r2 = r * r;
-  const uint32_t N = cfg->particle_count;
   const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
   const float vn = cfg->viscocity_kernel_norm;
   if (blockIdx.x == 0u && threadIdx.x == 0u) *sl.longq_n = 0u;  // the density pass's appends are done
-  __shared__ RunTable runs;
   __shared__ f4 terms[kBlock / 64u][64u * kLongSub];
   f4* const tb = terms[wv];
   f2* const tv = reinterpret_cast<f2*>(terms[wv]);
@@ -2666,9 +2690,9 @@ __global__ __launch_bounds__(kBlock) void sph_sim_long_kernel(const rps_config* 
     if (lane == 0u) sl.longq[k].x = 0u;  // cleared for the next active frame
     const uint32_t t = e.x - 1u;
     const f2 p = f2{__uint_as_float(e.y), __uint_as_float(e.z)};
-    uint32_t nr = 0;
-    const uint32_t total = nine_runs<LAYOUT>(rb, p[0], p[1], cfg->screen_bounds[1], cfg->screen_bounds[3], r, N, runs, &nr);
-    const RunRegs rr(runs, nr);
+    const uint2* tg = sl.longtab + (size_t)k * kLongTab;
+    const RunRegs rr(tg);
+    const uint32_t total = tg[9].y;
     const SimOwn o = sim_own(cfg, sl, t);
     const f4 own_pv = sl.rec_pv[t];
     if (kPads && !owner_is(sl, o.i, t)) continue;  // a repeat (wave-uniform)
@@ -2706,7 +2730,7 @@ __global__ __launch_bounds__(kBlock) void sph_sim_long_kernel(const rps_config* 
       for (uint32_t u = 0; u < kLongSub; ++u)
         cnt = long_compact(tb, cnt, in1[u], pressure_terms(q[u], p, o.P_rho2, o.Pn_rho2, r, dn, ndn));
       wave_lds_sync();
-      for (uint32_t i = 0; i < cnt; i += 8u) {
+      for (uint32_t i = 0; i < cnt && !(fx != fx && fy != fy); i += 8u) {  // (NaN: the scan stops)
         f4 w[8];
 #pragma unroll
         for (uint32_t j = 0; j < 8u; ++j) w[j] = tb[min(i + j, cnt - 1u)];
@@ -2732,7 +2756,7 @@ __global__ __launch_bounds__(kBlock) void sph_sim_long_kernel(const rps_config* 
         cnt = long_compact(tv, cnt, in[u], f2{(q[u][2] - qx) * kw, (q[u][3] - qy) * kw});
       }
       wave_lds_sync();
-      for (uint32_t i = 0; i < cnt; i += 8u) {
+      for (uint32_t i = 0; i < cnt && !(wx != wx && wy != wy); i += 8u) {
         f2 w[8];
 #pragma unroll
         for (uint32_t j = 0; j < 8u; ++j) w[j] = tv[min(i + j, cnt - 1u)];
