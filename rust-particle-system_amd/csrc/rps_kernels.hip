@@ -1991,6 +1991,35 @@ struct RunRegs {
 // count, compacted in entry order into the wave's LDS buffer, then read back by every lane
 // (broadcast reads, eight in flight) and added one entry after another -- the particle's own
 // order, as v_readlane per entry did at several times the cost.
+// Adds the compacted terms buf[0, cnt) to the pair s in order, each a pair (s += w) or, for
+// pressure's four-wide terms, two (s += w.xy, then s += w.zw): the reference's fx, fy updates,
+// as packed adds (per component IEEE, the same roundings).  Whole groups of eight go unguarded;
+// a sum NaN in both components stays NaN whatever follows, so the groups stop there.
+__device__ __forceinline__ void long_add(f2& s, const f2& w) { s = s + w; }
+__device__ __forceinline__ void long_add(f2& s, const f4& w) {
+  s = s + f2{w[0], w[1]};
+  s = s + f2{w[2], w[3]};
+}
+template <class T>
+__device__ __forceinline__ void long_sum(const T* buf, uint32_t cnt, f2& s) {
+  uint32_t i = 0;
+  for (; i + 8u <= cnt && !(s[0] != s[0] && s[1] != s[1]); i += 8u) {
+    T w[8];
+#pragma unroll
+    for (uint32_t j = 0; j < 8u; ++j) w[j] = buf[i + j];
+#pragma unroll
+    for (uint32_t j = 0; j < 8u; ++j) long_add(s, w[j]);
+  }
+  if (i < cnt && !(s[0] != s[0] && s[1] != s[1])) {  // the last group
+    T w[8];
+#pragma unroll
+    for (uint32_t j = 0; j < 8u; ++j) w[j] = buf[min(i + j, cnt - 1u)];
+#pragma unroll
+    for (uint32_t j = 0; j < 8u; ++j)
+      if (i + j < cnt) long_add(s, w[j]);
+  }
+}
+
 template <class T>
 __device__ __forceinline__ uint32_t long_compact(T* buf, uint32_t base, bool in, const T& w) {
   const uint64_t m = __builtin_amdgcn_ballot_w64(in);
@@ -2281,17 +2310,10 @@ __global__ __launch_bounds__(kBlock) void sph_density_long_kernel(const rps_conf
       }
       wave_lds_sync();
       // entries in increasing f: the lane's order; a sum NaN in both components stays NaN
-      for (uint32_t i = 0; i < cnt && !(d != d && nd != nd); i += 8u) {
-        f2 w[8];
-#pragma unroll
-        for (uint32_t j = 0; j < 8u; ++j) w[j] = terms[wv][min(i + j, cnt - 1u)];
-#pragma unroll
-        for (uint32_t j = 0; j < 8u; ++j)
-          if (i + j < cnt) {
-            d = d + w[j][0];
-            nd = nd + w[j][1];
-          }
-      }
+      f2 dd = f2{d, nd};
+      long_sum(terms[wv], cnt, dd);
+      d = dd[0];
+      nd = dd[1];
       wave_lds_sync();  // the next chunk rewrites the buffer
       if (d != d && nd != nd) break;  // NaN whatever follows (more than 128 entries: no mask)
     }
@@ -2730,19 +2752,10 @@ __global__ __launch_bounds__(kBlock) void sph_sim_long_kernel(const rps_config* 
       for (uint32_t u = 0; u < kLongSub; ++u)
         cnt = long_compact(tb, cnt, in1[u], pressure_terms(q[u], p, o.P_rho2, o.Pn_rho2, r, dn, ndn));
       wave_lds_sync();
-      for (uint32_t i = 0; i < cnt && !(fx != fx && fy != fy); i += 8u) {  // (NaN: the scan stops)
-        f4 w[8];
-#pragma unroll
-        for (uint32_t j = 0; j < 8u; ++j) w[j] = tb[min(i + j, cnt - 1u)];
-#pragma unroll
-        for (uint32_t j = 0; j < 8u; ++j)
-          if (i + j < cnt) {
-            fx = fx + w[j][0];
-            fy = fy + w[j][1];
-            fx = fx + w[j][2];
-            fy = fy + w[j][3];
-          }
-      }
+      f2 ff = f2{fx, fy};
+      long_sum(tb, cnt, ff);
+      fx = ff[0];
+      fy = ff[1];
       wave_lds_sync();
     }
     const float qx = own_pv[2] + fx * dt;
@@ -2756,17 +2769,10 @@ __global__ __launch_bounds__(kBlock) void sph_sim_long_kernel(const rps_config* 
         cnt = long_compact(tv, cnt, in[u], f2{(q[u][2] - qx) * kw, (q[u][3] - qy) * kw});
       }
       wave_lds_sync();
-      for (uint32_t i = 0; i < cnt && !(wx != wx && wy != wy); i += 8u) {
-        f2 w[8];
-#pragma unroll
-        for (uint32_t j = 0; j < 8u; ++j) w[j] = tv[min(i + j, cnt - 1u)];
-#pragma unroll
-        for (uint32_t j = 0; j < 8u; ++j)
-          if (i + j < cnt) {
-            wx = wx + w[j][0];
-            wy = wy + w[j][1];
-          }
-      }
+      f2 ww = f2{wx, wy};
+      long_sum(tv, cnt, ww);
+      wx = ww[0];
+      wy = ww[1];
       wave_lds_sync();
     };
     if (one) {
