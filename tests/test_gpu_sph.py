@@ -574,3 +574,65 @@ def test_sph_layout_clustered_runs(gpu, orc, monkeypatch):
             ctx.step(1)
             assert_bitwise(ctx.read_debug(rps.DEBUG_DENSITIES), st.dens, f"dens layout={layout}")
             assert_soa_bitwise(ctx.download_soa(), ref, what=f"clustered layout={layout} ")
+
+
+@pytest.mark.parametrize("n,env", [(2000, {}), (8192, {}), (10000, {}), (32768, {}),
+                                   (50000, {"RPS_SPH_CSORT_TLOG": "11"}), (50000, {"RPS_SPH_CSORT_TLOG": "13"}),
+                                   (65536, {"RPS_SPH_CSORT": "0"}), (65536, {"RPS_SPH_PAIRS": "0"})])
+def test_sph_compact_sort_shapes(gpu, orc, monkeypatch, n, env):
+    """The compact sort (2^11 <= P <= 2^16: 4-byte entries, every later stage's global passes
+    folded into its tail launch) at every shape it takes -- one launch (P = 2^11, 2^13), two and
+    three later stages (P = 2^14, 2^15), the forced 2048- and 8192-entry tiles at the reference
+    default (five / three later stages) --, and the frame with it and the lane-pair scans
+    switched off: three all-active frames, every pass bitwise (P != N included)."""
+    rps = gpu
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    cfg = rps.default_particle_config(n, gravity=100.0)
+    _frames_vs_oracle(rps, orc, n, _blob(n, n + 7), cfg, 3)
+
+
+@pytest.mark.parametrize("n", [50000, 8192])
+def test_sph_particle_order_bin_entries(gpu, orc, n):
+    """Without the layout the sim writes the next frame's bin entries (key, i), which the next
+    sort head reads instead of keying the positions: they must be dropped whenever the state or
+    the config changes between frames -- a field upload, a whole upload, a config change, a
+    gated frame after a config change -- and every frame stays bitwise."""
+    rps = gpu
+    cfg = rps.default_particle_config(n, gravity=100.0)
+    soa = _blob(n, 17)
+    st = orc.SphState(n)
+    ref = copy_soa(soa)
+
+    def frames(k, gated=0):
+        for f in range(k):
+            st.grid(cfg, ref)
+            if f >= gated:
+                st.pre(cfg, ref)
+                st.sim(cfg, ref)
+
+    with rps.Context(n, rps.MODE_SPH) as ctx:
+        ctx.set_config(cfg, rps.make_ext(shader_delay=0))
+        ctx.upload_soa(soa)
+        ctx.step(2)
+        frames(2)
+        x_new = (ref["x"][:500] * np.float32(0.75)).astype(F)
+        ctx.upload_field(rps.FIELD_X, x_new)
+        ref["x"][:500] = x_new
+        ctx.step(2)
+        frames(2)
+        assert_bitwise(ctx.read_debug(rps.DEBUG_SPATIAL_LOOKUP), st.lookup, "lookup after field upload")
+        assert_soa_bitwise(ctx.download_soa(), ref, what="after field upload ")
+        soa2 = _blob(n, 19)
+        ctx.upload_soa(soa2)
+        ref = copy_soa(soa2)
+        ctx.step(2)
+        frames(2)
+        assert_soa_bitwise(ctx.download_soa(), ref, what="after upload ")
+        cfg = rps.default_particle_config(n, gravity=70.0, smoothing_radius=9.0)
+        ctx.set_config(cfg, rps.make_ext(shader_delay=3))  # frame_count 0: frames 1, 2 gated
+        ctx.step(4)
+        frames(4, gated=2)
+        assert_bitwise(ctx.read_debug(rps.DEBUG_SPATIAL_LOOKUP), st.lookup, "lookup after config change")
+        assert_bitwise(ctx.read_debug(rps.DEBUG_LOOKUP_OFFSETS), st.offsets, "offsets after config change")
+        assert_soa_bitwise(ctx.download_soa(), ref, what="after config change ")
