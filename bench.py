@@ -430,9 +430,35 @@ def sph_side(rps, args, d):
                           "hbm_gbps_measured": hbm_frame / (frame_ms * 1e-3) / 1e9 if hbm_frame else None,
                           "hbm_frac_measured": hbm_frame / (frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS if hbm_frame else None,
                           "sort_launches": cost["sort_launches"]}}
+    out["reference_sizes"] = [sph_small(rps, args, d, m) for m in (50000, 65536)]
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline and args.sph_cpu_n > 0:
         out["cpu_baseline"] = sph_cpu_baseline(rps, args)
     return out
+
+
+def sph_small(rps, args, d, n):
+    """The SPH frame at the reference's own scale: its default N = 50 000 (src/main.rs:25; P =
+    2^16 with the pad entries of src/particle_buffers.rs:86) and 65 536, where launches and
+    latency, not bytes, set the frame time.  The reference dispatches 4 + S(S+1)/2 passes per
+    frame (S = log2 P; src/particle_compute.rs:105-191); `sort_launches` is this build's launch
+    count for the same network (the frame's other kernels: DESIGN.md §5.2)."""
+    cfg = rps.default_particle_config(n)
+    parts = rps.setup_particles_scatter(cfg, n, seed=args.seed)
+    frames = 200
+    ctx = rps.Context(n, rps.MODE_SPH, device=d.local if d.dist else 0)
+    try:
+        ctx.set_config(cfg, rps.make_ext(shader_delay=0))
+        ctx.upload(parts)
+        ctx.step(20)
+        ctx.sync()
+        ms = ctx.time_steps(frames) / frames
+        cost = ctx.sph_frame_cost()
+    finally:
+        ctx.close()
+    s = max(0, (n - 1).bit_length())
+    return {"particles": n, "frames": frames, "ms_per_frame": d.max(ms), "sort_launches": cost["sort_launches"],
+            "reference_dispatches_per_frame": 4 + s * (s + 1) // 2,
+            "timing": "one HIP event pair around the frames on the context stream (rps_time_steps), every frame active"}
 
 
 def sph_cpu_baseline(rps, args):
