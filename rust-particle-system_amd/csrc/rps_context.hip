@@ -56,6 +56,7 @@ struct rps_ctx {
   bool csort = true;      // RPS_SPH_CSORT: the compact sort at 2^11 <= P <= 2^16
   uint8_t csort_tlog = 0; // RPS_SPH_CSORT_TLOG (11..13; 0: by size)
   uint32_t pair_max_p = 0; // RPS_SPH_PAIRS: lane-pair scans up to this P
+  bool sim_fuse = true;    // RPS_SPH_SIM_FUSE: the sim and its long scans in one launch
   uint8_t sph_batch_d = 0, sph_batch_s = 0;  // forced scan batches (0: by size)
   SphLayoutArgs lay{};     // spatial record layout (RPS_SPH_LAYOUT, P >= 2^20 by default): arrays
   uint32_t cell_cap = 0;   // their cell capacity (0: no layout)
@@ -317,6 +318,7 @@ SphBuffers sph_buffers(rps_ctx* ctx) {
   b.csort = ctx->csort;
   b.csort_tlog = ctx->csort_tlog;
   b.pair_max_p = ctx->pair_max_p;
+  b.sim_fuse = ctx->sim_fuse;
   return b;
 }
 
@@ -635,6 +637,7 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     ctx->csort = env_int("RPS_SPH_CSORT", 1) != 0;
     ctx->csort_tlog = (uint8_t)std::max(0, std::min(13, env_int("RPS_SPH_CSORT_TLOG", 0)));
     ctx->pair_max_p = (uint32_t)std::max(0, env_int("RPS_SPH_PAIRS", 1 << 17));
+    ctx->sim_fuse = env_int("RPS_SPH_SIM_FUSE", 1) != 0;
     const int lay_mode = env_int("RPS_SPH_LAYOUT", 1);
     const bool lay_ok = lay_mode == 2 || (lay_mode == 1 && P >= (1u << 20));
     // With the layout the state is slot-resident (one entry per slot: P of them)

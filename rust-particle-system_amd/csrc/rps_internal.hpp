@@ -179,6 +179,7 @@ struct SphBuffers {
   bool csort;        // 2^11 <= P <= 2^16: the compact (4-byte entry) sort, RPS_SPH_CSORT
   uint8_t csort_tlog;  // its tile (11..13; 0: by size), RPS_SPH_CSORT_TLOG
   uint32_t pair_max_p;  // P <= this: density / sim scans by lane pairs (RPS_SPH_PAIRS)
+  bool sim_fuse;        // P != N: the sim and its long scans in one launch (RPS_SPH_SIM_FUSE)
   uint32_t cell_cap; // capacity of lay.cell_info / cellrun (0: layout never available)
   SphLayoutArgs lay;
 };

@@ -2280,7 +2280,8 @@ __global__ __launch_bounds__(kBlock) void sph_density2_kernel(const rps_config* 
 template <bool LAYOUT>
 __global__ __launch_bounds__(kBlock) void sph_density_long_kernel(const rps_config* __restrict__ cfg,
                                                                   RunBounds rb, SphSlots sl, uint32_t p_slots) {
-  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // uniform: the queue entry and its table go to SGPRs
   const uint32_t nw = gridDim.x * (kBlock / 64u);
   const float r = cfg->smoothing_radius, r2 = r * r;
   const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
@@ -2479,10 +2480,10 @@ __device__ __forceinline__ void sim_finish(const rps_config* __restrict__ cfg, c
 // to HBM as partial-line writes.  Slots the density pass queued (long scans)
 // are left to sph_sim_long_kernel.
 template <int kScanBatch, bool kPads, bool LAYOUT>
-__global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __restrict__ cfg,
-                                                         RunBounds rb, SphSlots sl, f4* __restrict__ st,
-                                                         uint2* __restrict__ bin_next, uint32_t p_slots) {
-  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+__device__ __forceinline__ void sim_body(const rps_config* __restrict__ cfg, const RunBounds& rb, const SphSlots& sl,
+                                         f4* __restrict__ st, uint2* __restrict__ bin_next, uint32_t p_slots,
+                                         uint32_t bid, RunTable& runs) {
+  const uint32_t t = bid * kBlock + threadIdx.x;
   if (t >= p_slots) return;
   const SimOwn o = sim_own(cfg, sl, t);
   if (kPads && !owner_is(sl, o.i, t)) return;  // a repeat: its owner slot computes the same state
@@ -2493,7 +2494,6 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
   const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
   const float vn = cfg->viscocity_kernel_norm;
   const f2 p = o.p;
-  __shared__ RunTable runs;
   const uint32_t total = nine_runs<LAYOUT>(rb, p[0], p[1], cfg->screen_bounds[1],
                                    cfg->screen_bounds[3], r, N, runs);
   const bool masked = total <= 128u;
@@ -2531,6 +2531,14 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
   else
     scan_runs<kScanBatch, kPads>(sl, runs, 0u, total, p, r2, self, load_pv, viscosity, viscosity_nan);
   sim_finish<LAYOUT>(cfg, sl, st, bin_next, t, o.i, qx, qy, wx, wy);
+}
+
+template <int kScanBatch, bool kPads, bool LAYOUT>
+__global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __restrict__ cfg,
+                                                         RunBounds rb, SphSlots sl, f4* __restrict__ st,
+                                                         uint2* __restrict__ bin_next, uint32_t p_slots) {
+  __shared__ RunTable runs;
+  sim_body<kScanBatch, kPads, LAYOUT>(cfg, rb, sl, st, bin_next, p_slots, blockIdx.x, runs);
 }
 
 // Lane-pair drivers of the sim's scans (see sph_density2_kernel): the entries split between the
@@ -2613,10 +2621,10 @@ __device__ __forceinline__ void scan_runs2(const SphSlots& sl, const RunTable& r
 
 // simulation_step (wgsl:435-453) by lane pairs; otherwise sph_sim_kernel.
 template <int kScanBatch, bool kPads, bool LAYOUT>
-__global__ __launch_bounds__(kBlock) void sph_sim2_kernel(const rps_config* __restrict__ cfg,
-                                                          RunBounds rb, SphSlots sl, f4* __restrict__ st,
-                                                          uint2* __restrict__ bin_next, uint32_t p_slots) {
-  const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
+__device__ __forceinline__ void sim2_body(const rps_config* __restrict__ cfg, const RunBounds& rb, const SphSlots& sl,
+                                          f4* __restrict__ st, uint2* __restrict__ bin_next, uint32_t p_slots,
+                                          uint32_t bid, RunTable& runs) {
+  const uint32_t g = bid * kBlock + threadIdx.x;
   const uint32_t t = g >> 1, par = g & 1u;
   if (t >= p_slots) return;
   const SimOwn o = sim_own(cfg, sl, t);
@@ -2628,7 +2636,6 @@ __global__ __launch_bounds__(kBlock) void sph_sim2_kernel(const rps_config* __re
   const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
   const float vn = cfg->viscocity_kernel_norm;
   const f2 p = o.p;
-  __shared__ RunTable runs;
   const uint32_t total = nine_runs<LAYOUT>(rb, p[0], p[1], cfg->screen_bounds[1],
                                    cfg->screen_bounds[3], r, N, runs);
   const bool masked = total <= 128u;
@@ -2689,24 +2696,33 @@ __global__ __launch_bounds__(kBlock) void sph_sim2_kernel(const rps_config* __re
   if (par == 0u) sim_finish<LAYOUT>(cfg, sl, st, bin_next, t, o.i, qx, qy, wx, wy);
 }
 
+template <int kScanBatch, bool kPads, bool LAYOUT>
+__global__ __launch_bounds__(kBlock) void sph_sim2_kernel(const rps_config* __restrict__ cfg,
+                                                          RunBounds rb, SphSlots sl, f4* __restrict__ st,
+                                                          uint2* __restrict__ bin_next, uint32_t p_slots) {
+  __shared__ RunTable runs;
+  sim2_body<kScanBatch, kPads, LAYOUT>(cfg, rb, sl, st, bin_next, p_slots, blockIdx.x, runs);
+}
+
 // The sim pass of the density pass's queued slots (kLongScan), one per wave: lane l evaluates
 // flat entries l, l + 64, ... of both scans; the sums add the lanes' terms entry by entry
 // (long_compact, then every lane reads them back in order).
+typedef f4 LongTerms[kBlock / 64u][64u * kLongSub];  // 16 KiB: fits a RunTable's 18 KiB
 template <bool kPads, bool LAYOUT>
-__global__ __launch_bounds__(kBlock) void sph_sim_long_kernel(const rps_config* __restrict__ cfg,
-                                                              RunBounds rb, SphSlots sl, f4* __restrict__ st,
-                                                              uint2* __restrict__ bin_next) {
-  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  const uint32_t nw = gridDim.x * (kBlock / 64u);
+__device__ __forceinline__ void sim_long_body(const rps_config* __restrict__ cfg, const RunBounds& rb,
+                                              const SphSlots& sl, f4* __restrict__ st, uint2* __restrict__ bin_next,
+                                              uint32_t bid, uint32_t nblk, LongTerms& terms) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // uniform: the queue entry and its table go to SGPRs
+  const uint32_t nw = nblk * (kBlock / 64u);
   const float dt = cfg->fixed_delta_time;
   const float r = cfg->smoothing_radius, r2 = r * r;
   const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
   const float vn = cfg->viscocity_kernel_norm;
-  if (blockIdx.x == 0u && threadIdx.x == 0u) *sl.longq_n = 0u;  // the density pass's appends are done
-  __shared__ f4 terms[kBlock / 64u][64u * kLongSub];
+  if (bid == 0u && threadIdx.x == 0u) *sl.longq_n = 0u;  // the density pass's appends are done
   f4* const tb = terms[wv];
   f2* const tv = reinterpret_cast<f2*>(terms[wv]);
-  for (uint32_t k = blockIdx.x * (kBlock / 64u) + wv;; k += nw) {
+  for (uint32_t k = bid * (kBlock / 64u) + wv;; k += nw) {
     const uint4 e = sl.longq[k];
     if (!e.x) break;  // past the last entry
     if (lane == 0u) sl.longq[k].x = 0u;  // cleared for the next active frame
@@ -2787,6 +2803,33 @@ __global__ __launch_bounds__(kBlock) void sph_sim_long_kernel(const rps_config* 
     }
     if (lane == 0u) sim_finish<LAYOUT>(cfg, sl, st, bin_next, t, o.i, qx, qy, wx, wy);
   }
+}
+
+template <bool kPads, bool LAYOUT>
+__global__ __launch_bounds__(kBlock) void sph_sim_long_kernel(const rps_config* __restrict__ cfg,
+                                                              RunBounds rb, SphSlots sl, f4* __restrict__ st,
+                                                              uint2* __restrict__ bin_next) {
+  __shared__ LongTerms terms;
+  sim_long_body<kPads, LAYOUT>(cfg, rb, sl, st, bin_next, blockIdx.x, gridDim.x, terms);
+}
+
+// The sim pass in one launch with the long scans (P != N): blocks [0, nlong) take the queued
+// slots (sim_long_body), the rest the slots in their lanes or lane pairs.  Neither part reads
+// what the other writes (states of disjoint particles; records and densities of the passes
+// before), so nothing orders them: the long slots' latency runs beside the main scans instead of
+// after them, and the frame loses a launch.
+template <int kScanBatch, bool kPads, bool LAYOUT, bool PAIRS>
+__global__ __launch_bounds__(kBlock) void sph_sim_fused_kernel(const rps_config* __restrict__ cfg,
+                                                               RunBounds rb, SphSlots sl, f4* __restrict__ st,
+                                                               uint2* __restrict__ bin_next, uint32_t p_slots,
+                                                               uint32_t nlong) {
+  __shared__ RunTable runs;
+  if (blockIdx.x < nlong) {
+    sim_long_body<kPads, LAYOUT>(cfg, rb, sl, st, bin_next, blockIdx.x, nlong, reinterpret_cast<LongTerms&>(runs));
+    return;
+  }
+  if constexpr (PAIRS) sim2_body<kScanBatch, kPads, LAYOUT>(cfg, rb, sl, st, bin_next, p_slots, blockIdx.x - nlong, runs);
+  else sim_body<kScanBatch, kPads, LAYOUT>(cfg, rb, sl, st, bin_next, p_slots, blockIdx.x - nlong, runs);
 }
 
 // predicted_positions / densities (wgsl:58, :61) rebuilt from the slot records for
@@ -3655,6 +3698,30 @@ hipError_t launch_sph_layout_pre(const SphBuffers& b, hipStream_t s) {
 
 hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s) {
   const RunBounds rb = run_bounds(b);
+  if (b.sl.longq && b.sim_fuse) {  // P != N: the long scans in the same launch (sph_sim_fused_kernel)
+    const uint32_t nlong = long_blocks(b.p);
+    const bool pairs = b.p <= b.pair_max_p;
+    const dim3 g(nlong + (pairs ? blocks_for(2u * b.p) : blocks_for(b.p)));
+#define RPS_SIMF(B, PR)                                                                                          \
+  if (b.layout)                                                                                                  \
+    hipLaunchKernelGGL((sph_sim_fused_kernel<B, true, true, PR>), g, dim3(kBlock), 0, s, b.cfg, rb, b.sl, b.st,    \
+                       b.bin_next, b.p, nlong);                                                                  \
+  else                                                                                                           \
+    hipLaunchKernelGGL((sph_sim_fused_kernel<B, true, false, PR>), g, dim3(kBlock), 0, s, b.cfg, rb, b.sl, b.st,   \
+                       b.bin_next, b.p, nlong)
+    if (pairs) {
+      if (b.batch_s == 4) { RPS_SIMF(4, true); } else { RPS_SIMF(2, true); }
+    } else {
+      switch (sph_batch(false, b.p, b.batch_s, b.layout)) {
+        case 4: RPS_SIMF(4, false); break;
+        case 6: RPS_SIMF(6, false); break;
+        case 16: RPS_SIMF(16, false); break;
+        default: RPS_SIMF(8, false); break;
+      }
+    }
+#undef RPS_SIMF
+    return hipGetLastError();
+  }
 #define RPS_SIM(B)                                                                                  \
   if (b.layout && b.p == b.n)                                                                       \
     hipLaunchKernelGGL((sph_sim_kernel<B, false, true>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s, \

@@ -578,13 +578,15 @@ def test_sph_layout_clustered_runs(gpu, orc, monkeypatch):
 
 @pytest.mark.parametrize("n,env", [(2000, {}), (8192, {}), (10000, {}), (32768, {}),
                                    (50000, {"RPS_SPH_CSORT_TLOG": "11"}), (50000, {"RPS_SPH_CSORT_TLOG": "13"}),
-                                   (65536, {"RPS_SPH_CSORT": "0"}), (65536, {"RPS_SPH_PAIRS": "0"})])
+                                   (65536, {"RPS_SPH_CSORT": "0"}), (65536, {"RPS_SPH_PAIRS": "0"}),
+                                   (50000, {"RPS_SPH_SIM_FUSE": "0"}), (50000, {"RPS_SPH_PAIRS": "0"})])
 def test_sph_compact_sort_shapes(gpu, orc, monkeypatch, n, env):
     """The compact sort (2^11 <= P <= 2^16: 4-byte entries, every later stage's global passes
     folded into its tail launch) at every shape it takes -- one launch (P = 2^11, 2^13), two and
     three later stages (P = 2^14, 2^15), the forced 2048- and 8192-entry tiles at the reference
-    default (five / three later stages) --, and the frame with it and the lane-pair scans
-    switched off: three all-active frames, every pass bitwise (P != N included)."""
+    default (five / three later stages) --, and the frame with it, the lane-pair scans and the
+    sim's fused long-scan blocks switched off: three all-active frames, every pass bitwise (P != N
+    included)."""
     rps = gpu
     for k, v in env.items():
         monkeypatch.setenv(k, v)
