@@ -28,6 +28,10 @@ for step in "$@"; do
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench)
       run bench 600 python bench.py || exit $? ;;
+    bench_driver)
+      run bench_driver 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 || exit $? ;;
+    prof_driver)
+      run prof_driver 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_driver -o run --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline || exit $? ;;
     bench_short)
       run bench_short 300 python bench.py --steps 50 --warmup 10 --no-cpu-baseline || exit $? ;;
     torchrun1)
