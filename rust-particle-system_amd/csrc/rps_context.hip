@@ -57,6 +57,7 @@ struct rps_ctx {
   uint8_t csort_tlog = 0; // RPS_SPH_CSORT_TLOG (11..13; 0: by size)
   uint32_t pair_max_p = 0; // RPS_SPH_PAIRS: lane-pair scans up to this P
   bool sim_fuse = true;    // RPS_SPH_SIM_FUSE: the sim and its long scans in one launch
+  uint8_t lane_group = 2;  // RPS_SPH_GROUP: lanes per slot of the small-P scans (2 or 4)
   uint8_t sph_batch_d = 0, sph_batch_s = 0;  // forced scan batches (0: by size)
   SphLayoutArgs lay{};     // spatial record layout (RPS_SPH_LAYOUT, P >= 2^20 by default): arrays
   uint32_t cell_cap = 0;   // their cell capacity (0: no layout)
@@ -319,6 +320,7 @@ SphBuffers sph_buffers(rps_ctx* ctx) {
   b.csort_tlog = ctx->csort_tlog;
   b.pair_max_p = ctx->pair_max_p;
   b.sim_fuse = ctx->sim_fuse;
+  b.lane_group = ctx->lane_group;
   return b;
 }
 
@@ -638,6 +640,13 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     ctx->csort_tlog = (uint8_t)std::max(0, std::min(13, env_int("RPS_SPH_CSORT_TLOG", 0)));
     ctx->pair_max_p = (uint32_t)std::max(0, env_int("RPS_SPH_PAIRS", 1 << 17));
     ctx->sim_fuse = env_int("RPS_SPH_SIM_FUSE", 1) != 0;
+    // Lanes per slot of the small-P scans: 4 below 65 536 particles (same box, ms/frame: 20 000
+    // 0.0561 -> 0.0531, 50 000 0.0883 -> 0.0863), 2 from there (65 536 0.0761 / 0.0769 with 4,
+    // 100 000 0.1215 / 0.1307); RPS_SPH_GROUP=2 or 4 forces one.
+    {
+      const int grp = env_int("RPS_SPH_GROUP", 0);
+      ctx->lane_group = grp == 2 || grp == 4 ? (uint8_t)grp : (n < 65536 ? 4 : 2);
+    }
     const int lay_mode = env_int("RPS_SPH_LAYOUT", 1);
     const bool lay_ok = lay_mode == 2 || (lay_mode == 1 && P >= (1u << 20));
     // With the layout the state is slot-resident (one entry per slot: P of them)

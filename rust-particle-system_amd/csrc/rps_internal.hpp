@@ -180,6 +180,7 @@ struct SphBuffers {
   uint8_t csort_tlog;  // its tile (11..13; 0: by size), RPS_SPH_CSORT_TLOG
   uint32_t pair_max_p;  // P <= this: density / sim scans by lane pairs (RPS_SPH_PAIRS)
   bool sim_fuse;        // P != N: the sim and its long scans in one launch (RPS_SPH_SIM_FUSE)
+  uint8_t lane_group;   // lanes per slot of those scans: 2 or 4 (RPS_SPH_GROUP)
   uint32_t cell_cap; // capacity of lay.cell_info / cellrun (0: layout never available)
   SphLayoutArgs lay;
 };

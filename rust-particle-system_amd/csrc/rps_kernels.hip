@@ -2204,19 +2204,26 @@ __global__ __launch_bounds__(kBlock) void sph_density_kernel(const rps_config* _
 // its partner's terms by DPP and BOTH add every entry in the reference's order (entry f + 2u,
 // then f + 2u + 1), so the pair holds identical sums, masks and loop conditions: the same
 // additions in the same order as one lane, twice the waves and half the chain per lane.
-__device__ __forceinline__ float pair_f(float v) {  // the partner lane's value (lane ^ 1)
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), kDppXor1, 0xF, 0xF, false));
+// Generalised to G = 2 or 4 lanes per slot (lane groups): lane `sub` of a group takes entries
+// f + G u + sub; every lane adds all G entries of each step in order, taking the others' terms by
+// a DPP broadcast inside the group, and the group's "entry counts" flags from one ballot.
+template <int G, int K>
+__device__ __forceinline__ float grp_bcast(float v) {  // lane K of this lane's group
+  constexpr int ctrl = G == 4 ? K * 0x55 : (K ? 0xF5 : 0xA0);  // quad_perm [K,K,K,K] / [K,K,K+2,K+2]
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), ctrl, 0xF, 0xF, false));
 }
-__device__ __forceinline__ uint32_t pair_u(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kDppXor1, 0xF, 0xF, false);
+template <int G>
+__device__ __forceinline__ uint32_t grp_flags(bool use) {  // bit k: lane k of the group's flag
+  const uint64_t m = __builtin_amdgcn_ballot_w64(use);
+  return (uint32_t)(m >> (threadIdx.x & 63u & ~(uint32_t)(G - 1))) & ((1u << G) - 1u);
 }
 
 // calculate_density (wgsl:207-254) by lane pairs; otherwise sph_density_kernel.
-template <int kScanBatch, bool LAYOUT>
+template <int kScanBatch, bool LAYOUT, int G>
 __global__ __launch_bounds__(kBlock) void sph_density2_kernel(const rps_config* __restrict__ cfg,
                                                               RunBounds rb, SphSlots sl, uint32_t p_slots) {
   const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
-  const uint32_t t = g >> 1, par = g & 1u;
+  const uint32_t t = g / G, par = g % G;
   if (t >= p_slots) return;  // pair-uniform, as every condition below
   const uint32_t N = cfg->particle_count;
   if (LAYOUT && par == 0u && t <= N / 32u) rb.keybits[t] = 0u;
@@ -2242,34 +2249,35 @@ __global__ __launch_bounds__(kBlock) void sph_density2_kernel(const rps_config* 
     }
   }
   const bool may_stop = own_finite || total > 128u;
-  for (uint32_t f = 0; f < total && !(may_stop && d != d && nd != nd); f += 2u * kScanBatch) {
+  for (uint32_t f = 0; f < total && !(may_stop && d != d && nd != nd); f += G * kScanBatch) {
     f2 q[kScanBatch];
 #pragma unroll
-    for (int u = 0; u < kScanBatch; ++u) q[u] = sl.pp_s[rc.slot_skip(min(f + 2u * u + par, total - 1u))];
+    for (int u = 0; u < kScanBatch; ++u) q[u] = sl.pp_s[rc.slot_skip(min(f + G * u + par, total - 1u))];
 #pragma unroll
     for (int u = 0; u < kScanBatch; ++u) {
-      const uint32_t b = f + 2u * u + par;  // this lane's entry
+      const uint32_t b = f + G * u + par;  // this lane's entry
       const float dx = p[0] - q[u][0], dy = p[1] - q[u][1];
       const float sq = dx * dx + dy * dy;
       const bool in = b < total && !(sq > r2);
       f2 k = f2{0.0f, 0.0f};
       if (in) k = density_terms(sq, r, dn, ndn);
-      const float k0o = pair_f(k[0]), k1o = pair_f(k[1]);
-      const bool ino = pair_u(in ? 1u : 0u) != 0u;
-      const bool ie = par ? ino : in, io = par ? in : ino;  // entries f + 2u (even), f + 2u + 1
-      if (ie) {
-        d = d + (par ? k0o : k[0]);
-        nd = nd + (par ? k1o : k[1]);
-      }
-      if (io) {
-        d = d + (par ? k[0] : k0o);
-        nd = nd + (par ? k[1] : k1o);
+      const uint32_t fl = grp_flags<G>(in);  // entries f + G u + 0 .. G - 1, in order
+      const auto add = [&](float a0, float a1, int kk) {
+        if ((fl >> kk) & 1u) {
+          d = d + a0;
+          nd = nd + a1;
+        }
+      };
+      add(grp_bcast<G, 0>(k[0]), grp_bcast<G, 0>(k[1]), 0);
+      add(grp_bcast<G, 1>(k[0]), grp_bcast<G, 1>(k[1]), 1);
+      if constexpr (G == 4) {
+        add(grp_bcast<G, 2>(k[0]), grp_bcast<G, 2>(k[1]), 2);
+        add(grp_bcast<G, 3>(k[0]), grp_bcast<G, 3>(k[1]), 3);
       }
       if (total <= 128u) {
-        const uint32_t be = f + 2u * u;
-        const uint64_t bits = (ie ? 1ull : 0ull) | (io ? 2ull : 0ull);
-        if (be < 64u) m0 |= bits << be;  // be is even: both bits in one word
-        else m1 |= bits << (be - 64u);
+        const uint32_t be = f + G * u;  // a multiple of G: the group's bits in one word
+        if (be < 64u) m0 |= (uint64_t)fl << be;
+        else m1 |= (uint64_t)fl << (be - 64u);
       }
     }
   }
@@ -2559,7 +2567,7 @@ __device__ __forceinline__ bool pop_bit(uint64_t& m0, uint64_t& m1, uint32_t& f)
   }
   return false;
 }
-template <int kScanBatch, bool kPads, class T, class Load, class Term, class Add, class Done>
+template <int kScanBatch, bool kPads, int G, class T, class Load, class Term, class Add, class Done>
 __device__ __forceinline__ void scan_masked2(const SphSlots& sl, const RunTable& runs, uint64_t m0, uint64_t m1,
                                              uint32_t self, uint32_t par, Load&& load, Term&& term, Add&& add,
                                              Done&& done) {
@@ -2570,13 +2578,25 @@ __device__ __forceinline__ void scan_masked2(const SphSlots& sl, const RunTable&
     bool live[kScanBatch];
     f4 q[kScanBatch];
 #pragma unroll
-    for (int u = 0; u < kScanBatch; ++u) {  // the next two set bits, lowest first: even, odd
-      uint32_t fe = 0u, fo = 0u;
-      const bool le = pop_bit(m0, m1, fe);
-      const bool lo = pop_bit(m0, m1, fo);
-      live[u] = par ? lo : le;
-      // an idle lane re-reads an entry it may read (the loop runs while the even lane has one)
-      fs[u] = live[u] ? (par ? fo : fe) : (le ? fe : prev);
+    for (int u = 0; u < kScanBatch; ++u) {  // the next G set bits, lowest first: lane k takes the k-th
+      uint32_t first = 0u, mine = 0u;
+      bool any = false, got = false;
+#pragma unroll
+      for (int kk = 0; kk < G; ++kk) {
+        uint32_t fb = 0u;
+        const bool lb = pop_bit(m0, m1, fb);
+        if (kk == 0) {
+          any = lb;
+          first = fb;
+        }
+        if ((uint32_t)kk == par) {
+          got = lb;
+          mine = fb;
+        }
+      }
+      live[u] = got;
+      // an idle lane re-reads an entry it may read (the loop runs while lane 0 has one)
+      fs[u] = got ? mine : (any ? first : prev);
       prev = fs[u];
     }
 #pragma unroll
@@ -2594,24 +2614,24 @@ __device__ __forceinline__ void scan_masked2(const SphSlots& sl, const RunTable&
     }
   }
 }
-template <int kScanBatch, bool kPads, class T, class Load, class Term, class Add, class Done>
+template <int kScanBatch, bool kPads, int G, class T, class Load, class Term, class Add, class Done>
 __device__ __forceinline__ void scan_runs2(const SphSlots& sl, const RunTable& runs, uint32_t total, f2 p, float r2,
                                            uint32_t self, uint32_t par, Load&& load, Term&& term, Add&& add,
                                            Done&& done) {
   RunCursor rc(runs);
-  for (uint32_t f = 0; f < total && !done(); f += 2u * kScanBatch) {
+  for (uint32_t f = 0; f < total && !done(); f += G * kScanBatch) {
     f4 q[kScanBatch];
     uint32_t qi[kScanBatch];
 #pragma unroll
     for (int u = 0; u < kScanBatch; ++u) {
-      const uint32_t j = rc.slot_skip(min(f + 2u * u + par, total - 1u));
+      const uint32_t j = rc.slot_skip(min(f + G * u + par, total - 1u));
       q[u] = load(j);
       qi[u] = kPads ? sl.idx_s[j] : j;
     }
 #pragma unroll
     for (int u = 0; u < kScanBatch; ++u) {
       const float dx = q[u][0] - p[0], dy = q[u][1] - p[1];
-      const bool use = f + 2u * u + par < total && qi[u] != self && !(dx * dx + dy * dy > r2);
+      const bool use = f + G * u + par < total && qi[u] != self && !(dx * dx + dy * dy > r2);
       T w{};
       if (use) w = term(q[u]);
       add(w, use, par);
@@ -2620,12 +2640,12 @@ __device__ __forceinline__ void scan_runs2(const SphSlots& sl, const RunTable& r
 }
 
 // simulation_step (wgsl:435-453) by lane pairs; otherwise sph_sim_kernel.
-template <int kScanBatch, bool kPads, bool LAYOUT>
+template <int kScanBatch, bool kPads, bool LAYOUT, int G>
 __device__ __forceinline__ void sim2_body(const rps_config* __restrict__ cfg, const RunBounds& rb, const SphSlots& sl,
                                           f4* __restrict__ st, uint2* __restrict__ bin_next, uint32_t p_slots,
                                           uint32_t bid, RunTable& runs) {
   const uint32_t g = bid * kBlock + threadIdx.x;
-  const uint32_t t = g >> 1, par = g & 1u;
+  const uint32_t t = g / G, par = g % G;
   if (t >= p_slots) return;
   const SimOwn o = sim_own(cfg, sl, t);
   if (kPads && !owner_is(sl, o.i, t)) return;
@@ -2644,28 +2664,28 @@ __device__ __forceinline__ void sim2_body(const rps_config* __restrict__ cfg, co
   float fx = 0.0f, fy = 0.0f;
   const auto load_pd = [&](uint32_t j) { return sl.rec_pd[j]; };
   const auto pterm = [&](const f4& q) { return pressure_terms(q, p, o.P_rho2, o.Pn_rho2, r, dn, ndn); };
-  const auto padd = [&](const f4& w, bool use, uint32_t pr) {
-    const f4 wo = f4{pair_f(w[0]), pair_f(w[1]), pair_f(w[2]), pair_f(w[3])};
-    const bool uo = pair_u(use ? 1u : 0u) != 0u;
-    const f4 we = pr ? wo : w, wd = pr ? w : wo;  // entries of the even lane, then the odd
-    if (pr ? uo : use) {
-      fx = fx + we[0];
-      fy = fy + we[1];
-      fx = fx + we[2];
-      fy = fy + we[3];
-    }
-    if (pr ? use : uo) {
-      fx = fx + wd[0];
-      fy = fy + wd[1];
-      fx = fx + wd[2];
-      fy = fy + wd[3];
+  const auto padd = [&](const f4& w, bool use, uint32_t) {
+    const uint32_t fl = grp_flags<G>(use);  // the group's entries of this step, lane 0's first
+    const auto add = [&](float a, float b, float c, float e, int kk) {
+      if ((fl >> kk) & 1u) {
+        fx = fx + a;
+        fy = fy + b;
+        fx = fx + c;
+        fy = fy + e;
+      }
+    };
+    add(grp_bcast<G, 0>(w[0]), grp_bcast<G, 0>(w[1]), grp_bcast<G, 0>(w[2]), grp_bcast<G, 0>(w[3]), 0);
+    add(grp_bcast<G, 1>(w[0]), grp_bcast<G, 1>(w[1]), grp_bcast<G, 1>(w[2]), grp_bcast<G, 1>(w[3]), 1);
+    if constexpr (G == 4) {
+      add(grp_bcast<G, 2>(w[0]), grp_bcast<G, 2>(w[1]), grp_bcast<G, 2>(w[2]), grp_bcast<G, 2>(w[3]), 2);
+      add(grp_bcast<G, 3>(w[0]), grp_bcast<G, 3>(w[1]), grp_bcast<G, 3>(w[2]), grp_bcast<G, 3>(w[3]), 3);
     }
   };
   const auto pressure_nan = [&] { return fx != fx && fy != fy; };
   if (masked)
-    scan_masked2<kScanBatch, kPads, f4>(sl, runs, m0, m1, self, par, load_pd, pterm, padd, pressure_nan);
+    scan_masked2<kScanBatch, kPads, G, f4>(sl, runs, m0, m1, self, par, load_pd, pterm, padd, pressure_nan);
   else
-    scan_runs2<kScanBatch, kPads, f4>(sl, runs, total, p, r2, self, par, load_pd, pterm, padd, pressure_nan);
+    scan_runs2<kScanBatch, kPads, G, f4>(sl, runs, total, p, r2, self, par, load_pd, pterm, padd, pressure_nan);
   const f4 own_pv = sl.rec_pv[t];
   const float qx = own_pv[2] + fx * dt;
   const float qy = own_pv[3] + fy * dt;
@@ -2675,33 +2695,35 @@ __device__ __forceinline__ void sim2_body(const rps_config* __restrict__ cfg, co
     const float k = viscosity_weight(q, p, r, vn);
     return f2{(q[2] - qx) * k, (q[3] - qy) * k};
   };
-  const auto vadd = [&](const f2& w, bool use, uint32_t pr) {
-    const f2 wo = f2{pair_f(w[0]), pair_f(w[1])};
-    const bool uo = pair_u(use ? 1u : 0u) != 0u;
-    const f2 we = pr ? wo : w, wd = pr ? w : wo;
-    if (pr ? uo : use) {
-      wx = wx + we[0];
-      wy = wy + we[1];
-    }
-    if (pr ? use : uo) {
-      wx = wx + wd[0];
-      wy = wy + wd[1];
+  const auto vadd = [&](const f2& w, bool use, uint32_t) {
+    const uint32_t fl = grp_flags<G>(use);
+    const auto add = [&](float a, float b, int kk) {
+      if ((fl >> kk) & 1u) {
+        wx = wx + a;
+        wy = wy + b;
+      }
+    };
+    add(grp_bcast<G, 0>(w[0]), grp_bcast<G, 0>(w[1]), 0);
+    add(grp_bcast<G, 1>(w[0]), grp_bcast<G, 1>(w[1]), 1);
+    if constexpr (G == 4) {
+      add(grp_bcast<G, 2>(w[0]), grp_bcast<G, 2>(w[1]), 2);
+      add(grp_bcast<G, 3>(w[0]), grp_bcast<G, 3>(w[1]), 3);
     }
   };
   const auto viscosity_nan = [&] { return wx != wx && wy != wy; };
   if (masked)
-    scan_masked2<kScanBatch, kPads, f2>(sl, runs, m0, m1, self, par, load_pv, vterm, vadd, viscosity_nan);
+    scan_masked2<kScanBatch, kPads, G, f2>(sl, runs, m0, m1, self, par, load_pv, vterm, vadd, viscosity_nan);
   else
-    scan_runs2<kScanBatch, kPads, f2>(sl, runs, total, p, r2, self, par, load_pv, vterm, vadd, viscosity_nan);
+    scan_runs2<kScanBatch, kPads, G, f2>(sl, runs, total, p, r2, self, par, load_pv, vterm, vadd, viscosity_nan);
   if (par == 0u) sim_finish<LAYOUT>(cfg, sl, st, bin_next, t, o.i, qx, qy, wx, wy);
 }
 
-template <int kScanBatch, bool kPads, bool LAYOUT>
+template <int kScanBatch, bool kPads, bool LAYOUT, int G>
 __global__ __launch_bounds__(kBlock) void sph_sim2_kernel(const rps_config* __restrict__ cfg,
                                                           RunBounds rb, SphSlots sl, f4* __restrict__ st,
                                                           uint2* __restrict__ bin_next, uint32_t p_slots) {
   __shared__ RunTable runs;
-  sim2_body<kScanBatch, kPads, LAYOUT>(cfg, rb, sl, st, bin_next, p_slots, blockIdx.x, runs);
+  sim2_body<kScanBatch, kPads, LAYOUT, G>(cfg, rb, sl, st, bin_next, p_slots, blockIdx.x, runs);
 }
 
 // The sim pass of the density pass's queued slots (kLongScan), one per wave: lane l evaluates
@@ -2818,7 +2840,7 @@ __global__ __launch_bounds__(kBlock) void sph_sim_long_kernel(const rps_config* 
 // what the other writes (states of disjoint particles; records and densities of the passes
 // before), so nothing orders them: the long slots' latency runs beside the main scans instead of
 // after them, and the frame loses a launch.
-template <int kScanBatch, bool kPads, bool LAYOUT, bool PAIRS>
+template <int kScanBatch, bool kPads, bool LAYOUT, int G>
 __global__ __launch_bounds__(kBlock) void sph_sim_fused_kernel(const rps_config* __restrict__ cfg,
                                                                RunBounds rb, SphSlots sl, f4* __restrict__ st,
                                                                uint2* __restrict__ bin_next, uint32_t p_slots,
@@ -2828,7 +2850,7 @@ __global__ __launch_bounds__(kBlock) void sph_sim_fused_kernel(const rps_config*
     sim_long_body<kPads, LAYOUT>(cfg, rb, sl, st, bin_next, blockIdx.x, nlong, reinterpret_cast<LongTerms&>(runs));
     return;
   }
-  if constexpr (PAIRS) sim2_body<kScanBatch, kPads, LAYOUT>(cfg, rb, sl, st, bin_next, p_slots, blockIdx.x - nlong, runs);
+  if constexpr (G > 1) sim2_body<kScanBatch, kPads, LAYOUT, G>(cfg, rb, sl, st, bin_next, p_slots, blockIdx.x - nlong, runs);
   else sim_body<kScanBatch, kPads, LAYOUT>(cfg, rb, sl, st, bin_next, p_slots, blockIdx.x - nlong, runs);
 }
 
@@ -3605,17 +3627,18 @@ static uint32_t long_blocks(uint32_t p) { return std::min<uint32_t>(blocks_for(p
 
 static hipError_t launch_sph_density(const SphBuffers& b, hipStream_t s) {
   const RunBounds rb = run_bounds(b);
-  if (b.p <= b.pair_max_p) {  // lane pairs (sph_density2_kernel)
-#define RPS_DENSITY2(B)                                                                              \
-  if (b.layout)                                                                                      \
-    hipLaunchKernelGGL((sph_density2_kernel<B, true>), dim3(blocks_for(2u * b.p)), dim3(kBlock), 0, s, \
-                       b.cfg, rb, b.sl, b.p);                                                         \
-  else                                                                                               \
-    hipLaunchKernelGGL((sph_density2_kernel<B, false>), dim3(blocks_for(2u * b.p)), dim3(kBlock), 0, s, \
+  if (b.p <= b.pair_max_p) {  // lane groups (sph_density2_kernel)
+#define RPS_DENSITY2(B, G)                                                                              \
+  if (b.layout)                                                                                         \
+    hipLaunchKernelGGL((sph_density2_kernel<B, true, G>), dim3(blocks_for(G * b.p)), dim3(kBlock), 0, s, \
+                       b.cfg, rb, b.sl, b.p);                                                            \
+  else                                                                                                  \
+    hipLaunchKernelGGL((sph_density2_kernel<B, false, G>), dim3(blocks_for(G * b.p)), dim3(kBlock), 0, s, \
                        b.cfg, rb, b.sl, b.p)
-    switch (b.batch_d) {
-      case 8: RPS_DENSITY2(8); break;
-      default: RPS_DENSITY2(4); break;
+    if (b.lane_group == 4) {
+      if (b.batch_d == 4) { RPS_DENSITY2(4, 4); } else { RPS_DENSITY2(2, 4); }
+    } else {
+      if (b.batch_d == 8) { RPS_DENSITY2(8, 2); } else { RPS_DENSITY2(4, 2); }
     }
 #undef RPS_DENSITY2
   } else {
@@ -3701,7 +3724,8 @@ hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s) {
   if (b.sl.longq && b.sim_fuse) {  // P != N: the long scans in the same launch (sph_sim_fused_kernel)
     const uint32_t nlong = long_blocks(b.p);
     const bool pairs = b.p <= b.pair_max_p;
-    const dim3 g(nlong + (pairs ? blocks_for(2u * b.p) : blocks_for(b.p)));
+    const uint32_t G = b.lane_group == 4 ? 4u : 2u;
+    const dim3 g(nlong + (pairs ? blocks_for(G * b.p) : blocks_for(b.p)));
 #define RPS_SIMF(B, PR)                                                                                          \
   if (b.layout)                                                                                                  \
     hipLaunchKernelGGL((sph_sim_fused_kernel<B, true, true, PR>), g, dim3(kBlock), 0, s, b.cfg, rb, b.sl, b.st,    \
@@ -3709,14 +3733,16 @@ hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s) {
   else                                                                                                           \
     hipLaunchKernelGGL((sph_sim_fused_kernel<B, true, false, PR>), g, dim3(kBlock), 0, s, b.cfg, rb, b.sl, b.st,   \
                        b.bin_next, b.p, nlong)
-    if (pairs) {
-      if (b.batch_s == 4) { RPS_SIMF(4, true); } else { RPS_SIMF(2, true); }
+    if (pairs && G == 4) {
+      if (b.batch_s == 2) { RPS_SIMF(2, 4); } else { RPS_SIMF(1, 4); }
+    } else if (pairs) {
+      if (b.batch_s == 4) { RPS_SIMF(4, 2); } else { RPS_SIMF(2, 2); }
     } else {
       switch (sph_batch(false, b.p, b.batch_s, b.layout)) {
-        case 4: RPS_SIMF(4, false); break;
-        case 6: RPS_SIMF(6, false); break;
-        case 16: RPS_SIMF(16, false); break;
-        default: RPS_SIMF(8, false); break;
+        case 4: RPS_SIMF(4, 1); break;
+        case 6: RPS_SIMF(6, 1); break;
+        case 16: RPS_SIMF(16, 1); break;
+        default: RPS_SIMF(8, 1); break;
       }
     }
 #undef RPS_SIMF
@@ -3735,22 +3761,23 @@ hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s) {
   else                                                                                              \
     hipLaunchKernelGGL((sph_sim_kernel<B, true, false>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s, \
                        b.cfg, rb, b.sl, b.st, b.bin_next, b.p)
-  if (b.p <= b.pair_max_p) {  // lane pairs (sph_sim2_kernel)
-#define RPS_SIM2(B)                                                                                          \
+  if (b.p <= b.pair_max_p) {  // lane groups (sph_sim2_kernel)
+#define RPS_SIM2(B, G)                                                                                       \
   {                                                                                                          \
-    const dim3 g2(blocks_for(2u * b.p));                                                                     \
+    const dim3 g2(blocks_for(G * b.p));                                                                      \
     if (b.layout && b.p == b.n)                                                                              \
-      hipLaunchKernelGGL((sph_sim2_kernel<B, false, true>), g2, dim3(kBlock), 0, s, b.cfg, rb, b.sl, b.st, b.bin_next, b.p); \
+      hipLaunchKernelGGL((sph_sim2_kernel<B, false, true, G>), g2, dim3(kBlock), 0, s, b.cfg, rb, b.sl, b.st, b.bin_next, b.p); \
     else if (b.layout)                                                                                       \
-      hipLaunchKernelGGL((sph_sim2_kernel<B, true, true>), g2, dim3(kBlock), 0, s, b.cfg, rb, b.sl, b.st, b.bin_next, b.p);  \
+      hipLaunchKernelGGL((sph_sim2_kernel<B, true, true, G>), g2, dim3(kBlock), 0, s, b.cfg, rb, b.sl, b.st, b.bin_next, b.p);  \
     else if (b.p == b.n)                                                                                     \
-      hipLaunchKernelGGL((sph_sim2_kernel<B, false, false>), g2, dim3(kBlock), 0, s, b.cfg, rb, b.sl, b.st, b.bin_next, b.p); \
+      hipLaunchKernelGGL((sph_sim2_kernel<B, false, false, G>), g2, dim3(kBlock), 0, s, b.cfg, rb, b.sl, b.st, b.bin_next, b.p); \
     else                                                                                                     \
-      hipLaunchKernelGGL((sph_sim2_kernel<B, true, false>), g2, dim3(kBlock), 0, s, b.cfg, rb, b.sl, b.st, b.bin_next, b.p); \
+      hipLaunchKernelGGL((sph_sim2_kernel<B, true, false, G>), g2, dim3(kBlock), 0, s, b.cfg, rb, b.sl, b.st, b.bin_next, b.p); \
   }
-    switch (b.batch_s) {
-      case 4: RPS_SIM2(4); break;
-      default: RPS_SIM2(2); break;
+    if (b.lane_group == 4) {
+      if (b.batch_s == 2) { RPS_SIM2(2, 4); } else { RPS_SIM2(1, 4); }
+    } else {
+      if (b.batch_s == 4) { RPS_SIM2(4, 2); } else { RPS_SIM2(2, 2); }
     }
 #undef RPS_SIM2
   } else {
