@@ -1500,12 +1500,12 @@ __device__ __forceinline__ void clds_chunk(uint32_t* lds, uint32_t t) {
   }
 }
 template <int LG>
-__device__ __forceinline__ void clds_chunks(uint32_t* lds, uint32_t t) {
+__device__ __forceinline__ void clds_chunks(uint32_t* lds, uint32_t t, bool active = true) {
   if constexpr (LG >= 4) {
     constexpr int K = LG - 3 >= 3 ? 3 : LG - 3;
-    clds_chunk<LG, K>(lds, t);
-    lds_sync<(2 << LG)>();
-    clds_chunks<LG - K>(lds, t);
+    if (active) clds_chunk<LG, K>(lds, t);
+    lds_sync<(2 << LG)>();  // every wave of the workgroup, active or not
+    clds_chunks<LG - K>(lds, t, active);
   }
 }
 template <int S>
@@ -1675,16 +1675,19 @@ __device__ __forceinline__ uint4 cfold4(const uint32_t* __restrict__ src, uint32
 // A later stage s = TLOG + TG - 1 of one tile: its TG global passes (cfold4, four consecutive
 // positions per thread and 16-B loads, through LDS to the tail's order) and its in-tile passes
 // (sph_sort_tail_kernel's schedule), src -> cout, or the uint2 lookup for the last stage.
-template <int TLOG, int TG, bool OUT_LOOKUP>
-__global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_eu(4))) void sph_csort_stage_kernel(
+// WIDE: twice the threads (TILE / 4), one cfold4 each, so a workgroup has twice the fold loads
+// in flight; the tail's in-tile passes then run on the first TILE / 8 threads (whole waves), the
+// others only joining the barriers.
+template <int TLOG, int TG, bool OUT_LOOKUP, bool WIDE = false>
+__global__ __launch_bounds__(1u << (TLOG - (WIDE ? 2 : 3))) __attribute__((amdgpu_waves_per_eu(4))) void sph_csort_stage_kernel(
     const uint32_t* __restrict__ src, uint32_t* __restrict__ cout, uint2* __restrict__ lookup) {
-  static_assert(TLOG >= 11 && TLOG <= 13 && TG >= 1 && TG <= 5, "compact sort shapes");
+  static_assert(TLOG >= 11 && TLOG <= 13 && TG >= 1 && TG <= 5 && (!WIDE || TLOG <= 12), "compact sort shapes");
   constexpr uint32_t TILE = 1u << TLOG, NT = TILE / 8;
   __shared__ uint32_t lds[TILE + TILE / 32];
   const uint32_t t = threadIdx.x;
   const uint32_t base0 = blockIdx.x * TILE;
 #pragma unroll
-  for (uint32_t k = 0; k < 2; ++k) {  // the folded entries 4 (t + k NT) .. + 3
+  for (uint32_t k = 0; k < (WIDE ? 1u : 2u); ++k) {  // the folded entries 4 (t + k NT) .. + 3
     const uint32_t q = 4u * (t + k * NT);
     const uint4 f = cfold4<TG>(src, base0 + q, TLOG);
     lds[padded(q)] = f.x;  // q = 0 mod 4: the four share one pad offset
@@ -1693,7 +1696,8 @@ __global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_e
     lds[padded(q) + 3u] = f.w;
   }
   __syncthreads();
-  {  // strides TILE/2, TILE/4, TILE/8 on the entries t + j * NT
+  const bool active = !WIDE || t < NT;
+  if (active) {  // strides TILE/2, TILE/4, TILE/8 on the entries t + j * NT
     const uint32_t a = padded(t);
     uint32_t v[8];
 #pragma unroll
@@ -1703,8 +1707,8 @@ __global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_e
     for (int j = 0; j < 8; ++j) lds[a + pad_off<NT>(j)] = v[j];
   }
   lds_sync<TILE>();
-  clds_chunks<TLOG - 4>(lds, t);
-  {  // strides 8, 4, 2, 1 (lane pair: stride 8 by DPP)
+  clds_chunks<TLOG - 4>(lds, t, active);
+  if (active) {  // strides 8, 4, 2, 1 (lane pair: stride 8 by DPP)
     const uint32_t a = padded(8u * t);
     uint32_t v[8];
 #pragma unroll
@@ -3438,11 +3442,14 @@ static hipError_t launch_sph_csort(const SphBuffers& b, const SortBin& bin, uint
   for (uint32_t stage = tl, k = 0; stage < stages; ++stage, ++k) {
     const uint32_t tg = stage - tl + 1u;
     const bool last = stage + 1u == stages;
+    const bool wide = b.csort_wide && tl <= 12u;
     const uint32_t* src = cb[k & 1u];
     uint32_t* dst = cb[(k + 1u) & 1u];
 #define RPS_CSTAGE(TL, TG)                                                                                        \
   case TG:                                                                                                        \
-    if (last) hipLaunchKernelGGL((sph_csort_stage_kernel<TL, TG, true>), dim3(tiles), dim3(nt), 0, s, src, dst, b.lookup); \
+    if (wide && last) hipLaunchKernelGGL((sph_csort_stage_kernel<TL, TG, true, (TL <= 12)>), dim3(tiles), dim3(2u * nt), 0, s, src, dst, b.lookup); \
+    else if (wide) hipLaunchKernelGGL((sph_csort_stage_kernel<TL, TG, false, (TL <= 12)>), dim3(tiles), dim3(2u * nt), 0, s, src, dst, b.lookup); \
+    else if (last) hipLaunchKernelGGL((sph_csort_stage_kernel<TL, TG, true>), dim3(tiles), dim3(nt), 0, s, src, dst, b.lookup); \
     else hipLaunchKernelGGL((sph_csort_stage_kernel<TL, TG, false>), dim3(tiles), dim3(nt), 0, s, src, dst, b.lookup); \
     break
     switch (tl) {
