@@ -55,7 +55,7 @@ struct rps_ctx {
   bool sort_fold = true;  // RPS_SPH_SORT_FOLD (rps_kernels.hip, launch_sph_sort)
   bool csort = true;      // RPS_SPH_CSORT: the compact sort at 2^11 <= P <= 2^16
   uint8_t csort_tlog = 0; // RPS_SPH_CSORT_TLOG (11..13; 0: by size)
-  bool csort_wide = true; // RPS_SPH_CSORT_WIDE
+  uint8_t csort_wide = 4; // RPS_SPH_CSORT_WIDE
   uint32_t pair_max_p = 0; // RPS_SPH_PAIRS: lane-pair scans up to this P
   bool sim_fuse = true;    // RPS_SPH_SIM_FUSE: the sim and its long scans in one launch
   uint8_t lane_group = 2;  // RPS_SPH_GROUP: lanes per slot of the small-P scans (2 or 4)
@@ -640,7 +640,7 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     ctx->sort_fold = env_int("RPS_SPH_SORT_FOLD", 1) != 0;
     ctx->csort = env_int("RPS_SPH_CSORT", 1) != 0;
     ctx->csort_tlog = (uint8_t)std::max(0, std::min(13, env_int("RPS_SPH_CSORT_TLOG", 0)));
-    ctx->csort_wide = env_int("RPS_SPH_CSORT_WIDE", 1) != 0;
+    ctx->csort_wide = (uint8_t)std::max(0, std::min(5, env_int("RPS_SPH_CSORT_WIDE", 4)));
     ctx->pair_max_p = (uint32_t)std::max(0, env_int("RPS_SPH_PAIRS", 1 << 17));
     ctx->sim_fuse = env_int("RPS_SPH_SIM_FUSE", 1) != 0;
     // Lanes per slot of the small-P scans: 4 below 65 536 particles (same box, ms/frame: 20 000

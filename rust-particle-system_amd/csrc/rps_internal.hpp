@@ -178,7 +178,7 @@ struct SphBuffers {
   bool sort_fold;    // the first two later sort stages fold their global passes into the tails
   bool csort;        // 2^11 <= P <= 2^16: the compact (4-byte entry) sort, RPS_SPH_CSORT
   uint8_t csort_tlog;  // its tile (11..13; 0: by size), RPS_SPH_CSORT_TLOG
-  bool csort_wide;     // its later stages fold with twice the threads (RPS_SPH_CSORT_WIDE)
+  uint8_t csort_wide;  // its stages of this many folded passes or more fold with twice the threads (0: none), RPS_SPH_CSORT_WIDE
   uint32_t pair_max_p;  // P <= this: density / sim scans by lane pairs (RPS_SPH_PAIRS)
   bool sim_fuse;        // P != N: the sim and its long scans in one launch (RPS_SPH_SIM_FUSE)
   uint8_t lane_group;   // lanes per slot of those scans: 2 or 4 (RPS_SPH_GROUP)

@@ -3442,7 +3442,7 @@ static hipError_t launch_sph_csort(const SphBuffers& b, const SortBin& bin, uint
   for (uint32_t stage = tl, k = 0; stage < stages; ++stage, ++k) {
     const uint32_t tg = stage - tl + 1u;
     const bool last = stage + 1u == stages;
-    const bool wide = b.csort_wide && tl <= 12u;
+    const bool wide = b.csort_wide && tl <= 12u && tg >= b.csort_wide;  // the wide fold pays from 4 folded passes on
     const uint32_t* src = cb[k & 1u];
     uint32_t* dst = cb[(k + 1u) & 1u];
 #define RPS_CSTAGE(TL, TG)                                                                                        \

@@ -581,7 +581,7 @@ def test_sph_layout_clustered_runs(gpu, orc, monkeypatch):
                                    (65536, {"RPS_SPH_CSORT": "0"}), (65536, {"RPS_SPH_PAIRS": "0"}),
                                    (50000, {"RPS_SPH_SIM_FUSE": "0"}), (50000, {"RPS_SPH_PAIRS": "0"}),
                                    (50000, {"RPS_SPH_GROUP": "2"}), (65536, {"RPS_SPH_GROUP": "4"}),
-                                   (100000, {"RPS_SPH_GROUP": "4"}), (65536, {"RPS_SPH_CSORT_WIDE": "0"}),
+                                   (100000, {"RPS_SPH_GROUP": "4"}), (65536, {"RPS_SPH_CSORT_WIDE": "0"}), (32768, {"RPS_SPH_CSORT_WIDE": "1"}),
                                    (50000, {"RPS_SPH_CSORT_WIDE": "0", "RPS_SPH_CSORT_TLOG": "11"})])
 def test_sph_compact_sort_shapes(gpu, orc, monkeypatch, n, env):
     """The compact sort (2^11 <= P <= 2^16: 4-byte entries, every later stage's global passes
