@@ -59,6 +59,7 @@ struct rps_ctx {
   uint32_t pair_max_p = 0; // RPS_SPH_PAIRS: lane-pair scans up to this P
   bool sim_fuse = true;    // RPS_SPH_SIM_FUSE: the sim and its long scans in one launch
   uint8_t lane_group = 2;  // RPS_SPH_GROUP: lanes per slot of the small-P scans (2 or 4)
+  uint8_t lane_group_s = 2;  // RPS_SPH_GROUP_S: the sim's (default: lane_group)
   uint8_t sph_batch_d = 0, sph_batch_s = 0;  // forced scan batches (0: by size)
   SphLayoutArgs lay{};     // spatial record layout (RPS_SPH_LAYOUT, P >= 2^20 by default): arrays
   uint32_t cell_cap = 0;   // their cell capacity (0: no layout)
@@ -323,6 +324,7 @@ SphBuffers sph_buffers(rps_ctx* ctx) {
   b.pair_max_p = ctx->pair_max_p;
   b.sim_fuse = ctx->sim_fuse;
   b.lane_group = ctx->lane_group;
+  b.lane_group_s = ctx->lane_group_s;
   return b;
 }
 
@@ -649,6 +651,8 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     {
       const int grp = env_int("RPS_SPH_GROUP", 0);
       ctx->lane_group = grp == 2 || grp == 4 ? (uint8_t)grp : (n < 65536 ? 4 : 2);
+      const int gs = env_int("RPS_SPH_GROUP_S", 0);
+      ctx->lane_group_s = gs == 2 || gs == 4 ? (uint8_t)gs : ctx->lane_group;
     }
     const int lay_mode = env_int("RPS_SPH_LAYOUT", 1);
     const bool lay_ok = lay_mode == 2 || (lay_mode == 1 && P >= (1u << 20));

@@ -582,7 +582,9 @@ def test_sph_layout_clustered_runs(gpu, orc, monkeypatch):
                                    (50000, {"RPS_SPH_SIM_FUSE": "0"}), (50000, {"RPS_SPH_PAIRS": "0"}),
                                    (50000, {"RPS_SPH_GROUP": "2"}), (65536, {"RPS_SPH_GROUP": "4"}),
                                    (100000, {"RPS_SPH_GROUP": "4"}), (65536, {"RPS_SPH_CSORT_WIDE": "0"}), (32768, {"RPS_SPH_CSORT_WIDE": "1"}),
-                                   (50000, {"RPS_SPH_CSORT_WIDE": "0", "RPS_SPH_CSORT_TLOG": "11"})])
+                                   (50000, {"RPS_SPH_CSORT_WIDE": "0", "RPS_SPH_CSORT_TLOG": "11"}),
+                                   (50000, {"RPS_SPH_BATCH_S": "1"}), (50000, {"RPS_SPH_GROUP_S": "2"}),
+                                   (20000, {"RPS_SPH_GROUP": "2", "RPS_SPH_GROUP_S": "4", "RPS_SPH_SIM_FUSE": "0"})])
 def test_sph_compact_sort_shapes(gpu, orc, monkeypatch, n, env):
     """The compact sort (2^11 <= P <= 2^16: 4-byte entries, every later stage's global passes
     folded into its tail launch) at every shape it takes -- one launch (P = 2^11, 2^13), two and
