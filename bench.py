@@ -669,8 +669,12 @@ def main():
                      "frac": achieved / HBM_PEAK_GBPS,
                      "traffic": traffic, "kernel": "stream_step_kernel<euler,lifetime>",
                      "avg_kernel_ms": kern_ms, "launches": args.steps,
+                     "avg_step_gpu_ms": kern_ms,
+                     "stats_steps_in_region": sum(1 for k in range(args.warmup, args.warmup + args.steps)
+                                                  if k % max(1, getattr(ext, "stats_interval", 100)) == 0),
                      "timing": "one HIP event pair on the context stream around the K timed launches "
-                               "(includes the stats fold of any 100th step in the region); max over ranks",
+                               "(includes the stats fold of any 100th step in the region, counted in "
+                               "stats_steps_in_region; avg_kernel_ms = avg_step_gpu_ms = span / K); max over ranks",
                      "bytes_per_launch": moved_per_launch,
                      "bytes_basis": "bytes the kernel moves (rps_step_cost: 32.03 B per particle; PMC agrees "
                                     "within 0.3 %, profiles/pmc_traffic.json)",
