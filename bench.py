@@ -206,11 +206,12 @@ def global_stats(d, st):
 
 def pmc_traffic(workload_name, n_rank):
     """The dominant kernel's HBM bytes per launch from the committed PMC run of this workload
-    (profiles/pmc_traffic.json, tools/pmc_table.py), when that run processed the same number of
-    particles per launch as this rank; None otherwise (shards of another size)."""
+    (profiles/pmc_traffic.json, tools/pmc_table.py, keyed by the workload name, which carries the
+    global particle count), when that run processed the same number of particles per launch as
+    this rank; None otherwise (another workload, or shards of another size)."""
     try:
         with open(PMC_FILE) as f:
-            rec = json.load(f).get("C3-1e8-4att-drag-respawn-euler", {})
+            rec = json.load(f).get(workload_name, {})
     except (OSError, ValueError):
         return None
     if not rec or rec.get("particles_per_launch", 100_000_000) != n_rank:
@@ -395,14 +396,22 @@ def sph_side(rps, args, d):
         ctx.close()
     sim_ms = d.max(sim_ms)
     frame_ms = el * 1e3 / args.sph_frames
-    sim_gbps = cost["sim_bytes"] / (sim_ms * 1e-3) / 1e9
+    sim_algo_gbps = cost["sim_bytes"] / (sim_ms * 1e-3) / 1e9
     # Measured traffic (PMC, the bench workload at 2^22; profiles/pmc_traffic.json): the sim
-    # kernel's L1 -> L2 request bytes, and every SPH kernel's memory-side bytes per frame.
+    # kernel's L1 -> L2 request bytes and memory-side bytes per launch, and every SPH kernel's
+    # memory-side bytes per frame.  `frac` is a utilisation: the measured L1 -> L2 bytes' rate
+    # against the aggregate L2 peak (the scans' gathers are mostly L1 hits, so the algorithmic
+    # bytes -- every neighbour gather charged -- only give an equivalence rate).
     pmc = pmc_sph() if n == 1 << 22 else None
     pmc_src = f"profiles/pmc_traffic.json 'SPH-2^22-frame' (round {pmc.get('round')}; not this run)" if pmc else None
-    sim_pmc = next((v for k, v in (pmc or {}).get("per_dispatch", {}).items() if k.startswith("sph_sim_kernel")), None)
-    sim_traffic = sim_pmc["l2_read_bytes"] + sim_pmc["l2_write_bytes"] if sim_pmc else None
+    sim_name, sim_pmc = next(((k, v) for k, v in (pmc or {}).get("per_dispatch", {}).items()
+                              if k.startswith("sph_sim")), (None, None))
+    sim_l2 = sim_pmc["l2_read_bytes"] + sim_pmc["l2_write_bytes"] if sim_pmc else None
+    sim_hbm = sim_pmc.get("hbm_bytes") if sim_pmc else None
+    rate = lambda b, ms: b / (ms * 1e-3) / 1e9 if b else None  # noqa: E731
+    frac = lambda b, ms, peak: rate(b, ms) / peak if b else None  # noqa: E731
     hbm_frame = (pmc or {}).get("frame_sum_of_kernels", {}).get("hbm_bytes")
+    l2_frame = (pmc or {}).get("frame_sum_of_kernels", {}).get("l2_bytes")
     slots = 1 << max(0, (n - 1).bit_length())  # P = next_pow2(N) (particle_buffers.rs:86)
     layout = os.environ.get("RPS_SPH_LAYOUT", "1")
     spatial = layout == "2" or (layout == "1" and slots >= (1 << 20))  # rps_context.hip
@@ -411,25 +420,30 @@ def sph_side(rps, args, d):
            "scaling": "replicas", "frames": args.sph_frames, "ms_per_frame": frame_ms,
            "particle_steps_per_s": float(n) * d.world * args.sph_frames / el,
            "sim_kernel_ms": sim_ms,
-           "roofline": {"bound": "l2", "kernel": "sph_sim_kernel", "achieved": sim_gbps, "peak": L2_PEAK_GBPS,
-                        "unit": "GB/s", "frac": sim_gbps / L2_PEAK_GBPS, "traffic": sim_traffic,
-                        "traffic_gbps": sim_traffic / (sim_ms * 1e-3) / 1e9 if sim_traffic else None,
-                        "traffic_frac": sim_traffic / (sim_ms * 1e-3) / 1e9 / L2_PEAK_GBPS if sim_traffic else None,
+           "roofline": {"bound": "l2", "kernel": sim_name or "sph_sim_kernel",
+                        "achieved": rate(sim_l2, sim_ms), "peak": L2_PEAK_GBPS, "unit": "GB/s",
+                        "frac": frac(sim_l2, sim_ms, L2_PEAK_GBPS), "traffic": sim_l2,
+                        "hbm_bytes_per_launch": sim_hbm, "hbm_gbps": rate(sim_hbm, sim_ms),
+                        "hbm_frac": frac(sim_hbm, sim_ms, HBM_PEAK_GBPS),
                         "traffic_source": pmc_src,
                         "algorithmic_bytes_per_launch": cost["sim_bytes"],
+                        "algorithmic_equiv_gbps": sim_algo_gbps,
+                        "algorithmic_equiv_frac": sim_algo_gbps / L2_PEAK_GBPS,
                         "scanned_entries_per_particle": cost["scanned_entries"] / cost["slots"],
                         "within_radius_per_particle": cost["within_entries"] / cost["slots"],
-                        "note": "achieved/frac: the algorithmic bytes (every neighbour gather charged; most are "
-                                "served by the L1s) per kernel time, as a rate against the aggregate L2 peak -- "
-                                "not an L2 utilisation; traffic: the L1 -> L2 request bytes the PMC counters "
-                                "measured per launch (profiles/pmc_traffic.json), traffic_frac its rate against "
-                                "the same peak"},
-           "frame_cost": {"bytes": cost["frame_bytes"], "gbps": cost["frame_bytes"] / (frame_ms * 1e-3) / 1e9,
-                          "frac_of_l2": cost["frame_bytes"] / (frame_ms * 1e-3) / 1e9 / L2_PEAK_GBPS,
-                          "hbm_bytes_measured": hbm_frame, "hbm_bytes_source": pmc_src,
-                          "hbm_gbps_measured": hbm_frame / (frame_ms * 1e-3) / 1e9 if hbm_frame else None,
-                          "hbm_frac_measured": hbm_frame / (frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS if hbm_frame else None,
-                          "sort_launches": cost["sort_launches"]}}
+                        "note": "achieved/frac: the sim kernel's L1 -> L2 request bytes measured by the PMC "
+                                "counters (traffic, per launch) / this run's kernel time, against the aggregate "
+                                "L2 peak; hbm_frac: its memory-side bytes against HBM; algorithmic_equiv_*: every "
+                                "neighbour gather charged (mostly L1 hits) -- an equivalence, not a utilisation"},
+           "frame_cost": {"hbm_bytes_measured": hbm_frame, "hbm_bytes_source": pmc_src,
+                          "hbm_gbps": rate(hbm_frame, frame_ms), "frac": frac(hbm_frame, frame_ms, HBM_PEAK_GBPS),
+                          "bound": "hbm", "peak": HBM_PEAK_GBPS,
+                          "l2_bytes_measured": l2_frame, "l2_frac": frac(l2_frame, frame_ms, L2_PEAK_GBPS),
+                          "algorithmic_bytes": cost["frame_bytes"],
+                          "algorithmic_equiv_frac_of_l2": cost["frame_bytes"] / (frame_ms * 1e-3) / 1e9 / L2_PEAK_GBPS,
+                          "sort_launches": cost["sort_launches"],
+                          "note": "frac: the frame's memory-side bytes (sum over its kernels, PMC) per frame time "
+                                  "against HBM"}}
     out["reference_sizes"] = [sph_small(rps, args, d, m) for m in (50000, 65536)]
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline and args.sph_cpu_n > 0:
         out["cpu_baseline"] = sph_cpu_baseline(rps, args)
@@ -638,6 +652,12 @@ def main():
         stats, stats_ok = stats_check(d, ctx.stats(), ctx.shard_stats())
     else:
         stats, stats_ok = global_stats(d, ctx.stats()), True
+    # The last stats step (every stats_interval-th active step) is the one reported: a step of the
+    # timed region when one fell in it, else a warm-up step (the driver's --warmup 5 --steps 20).
+    first_timed = args.warmup
+    stats["when"] = ("timed region" if stats["step"] >= first_timed else
+                     f"warm-up step {stats['step']} (no stats step among the timed steps "
+                     f"{first_timed}..{first_timed + args.steps - 1})")
     ctx.close()
 
     updates = float(n_global) * args.steps
@@ -686,6 +706,12 @@ def main():
                              "algorithmic_equiv_gbps is the 40-B rate, an equivalence, not traffic"},
         "stats": stats,
     }
+    # The per-rank state (16 B per particle + the expiry arrays) against the 256-MB Infinity Cache
+    # (MI355X_MICROARCH.md): when it fits, FETCH_SIZE counts cache hits and the "HBM" rate is
+    # not DRAM traffic alone (the strong-scaled 8-GPU shard: 200 MB).
+    state_bytes = 16.0 * n_max + 2.0 * n_max + 2.0 * n_max / 64.0
+    line["roofline"]["state_bytes_per_rank"] = state_bytes
+    line["roofline"]["infinity_cache_resident"] = state_bytes <= 256 * 1024 * 1024
     if export is not None:
         line["export"] = export
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:

@@ -481,7 +481,9 @@ int sph_canonical(rps_ctx* ctx) {
   if (!ctx->resident) return RPS_OK;
   const SphBuffers b = sph_buffers(ctx);
   RPS_HIP(ctx, launch_sph_materialize(b, ctx->st, ctx->sl.idx_s, ctx->st_alt, ctx->stream));
-  RPS_HIP(ctx, launch_sph_pad_unflag(b, ctx->stream));  // P != N: pad payloads back to indices
+  // The lookup's payloads back to particle indices (slots of lookup_perm; P != N: flagged pads).
+  RPS_HIP(ctx, launch_sph_lookup_canonical(b, ctx->lookup_perm, ctx->stream));
+  ctx->lookup_perm = nullptr;
   std::swap(ctx->st, ctx->st_alt);
   set_sph_fields(ctx);
   ctx->resident = false;
@@ -535,6 +537,11 @@ int step_sph_sim(rps_ctx* ctx, bool layout, const SphGrid& g) {
 extern "C" {
 
 uint32_t rps_abi_version(void) { return RPS_ABI_VERSION; }
+
+#ifndef RPS_BUILD_ID
+#define RPS_BUILD_ID "unknown"
+#endif
+const char* rps_build_id(void) { return RPS_BUILD_ID; }
 
 const char* rps_status_string(int status) {
   switch (status) {

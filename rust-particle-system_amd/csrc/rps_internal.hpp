@@ -213,7 +213,8 @@ hipError_t launch_sph_debug_views(const SphBuffers& b, hipStream_t s);
 // particle order (dst[perm[u]] = st[u]), and the sorted lookup's payloads as particle indices.
 hipError_t launch_sph_rebin(const SphBuffers& b, const uint32_t* perm, hipStream_t s);
 hipError_t launch_sph_materialize(const SphBuffers& b, const f4* st, const uint32_t* perm, f4* dst, hipStream_t s);
-hipError_t launch_sph_pad_unflag(const SphBuffers& b, hipStream_t s);
+// The lookup's payloads as particle indices in place (slots through perm, flagged pads unflagged).
+hipError_t launch_sph_lookup_canonical(const SphBuffers& b, const uint32_t* perm, hipStream_t s);
 hipError_t launch_sph_lookup_translate(const uint2* lookup, const uint32_t* perm, uint2* out, uint32_t p,
                                        hipStream_t s);
 

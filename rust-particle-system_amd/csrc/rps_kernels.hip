@@ -2899,11 +2899,16 @@ __global__ __launch_bounds__(kBlock) void sph_materialize_kernel(const f4* __res
   const uint32_t u = blockIdx.x * kBlock + threadIdx.x;
   if (u < slots && (!sl.owner || owner_is(sl, perm[u], u))) dst[perm[u]] = st[u];
 }
-// Leaving slot-resident state with P != N: the pad entries' payloads back to plain indices.
-__global__ __launch_bounds__(kBlock) void sph_pad_unflag_kernel(uint2* __restrict__ lookup, uint32_t n,
-                                                                uint32_t p) {
-  const uint32_t k = n + blockIdx.x * kBlock + threadIdx.x;
-  if (k < p) lookup[k].y &= ~kPidFlag;
+// Leaving slot-resident state: the lookup's payloads back to particle indices in place -- the
+// slots [0, N) name through `perm` (null: already indices) and, with P != N, the pad entries'
+// flagged indices -- so the lookup is the reference's spatial_lookup again and no later read
+// needs the slot map (rps_read_debug after a download / export / upload).
+__global__ __launch_bounds__(kBlock) void sph_lookup_canonical_kernel(uint2* lookup, const uint32_t* __restrict__ perm,
+                                                                      uint32_t p) {
+  const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
+  if (k >= p) return;
+  const uint32_t y = lookup[k].y;
+  lookup[k].y = (y & kPidFlag) ? y & ~kPidFlag : perm ? perm[y] : y;
 }
 // The sorted lookup with particle indices as payloads (the reference's spatial_lookup).
 __global__ __launch_bounds__(kBlock) void sph_lookup_translate_kernel(const uint2* __restrict__ lookup,
@@ -3473,10 +3478,11 @@ static hipError_t launch_sph_csort(const SphBuffers& b, const SortBin& bin, uint
   return hipSuccess;
 }
 
-// Whether this frame's sort runs compact: 2^11 <= P <= 2^16 and every lookup payload below 2^16
-// (pad entries of a layout frame with P != N carry kPidFlag).
+// Whether this frame's sort runs compact: 2^11 <= P <= 2^16 and every lookup payload below 2^16.
+// Only a resident frame with P != N holds flagged payloads (the pad entries the previous layout
+// frame wrote); sph_canonical unflags them before any frame that leaves the layout.
 static bool csort_ok(const SphBuffers& b) {
-  return b.csort && b.p >= 2048u && b.p <= 65536u && (b.p == b.n || b.cell_cap == 0u);
+  return b.csort && b.p >= 2048u && b.p <= 65536u && !(b.resident && b.p != b.n);
 }
 
 // Passes 1-2 of the frame: bin (folded into the first sort launch) + the bitonic network.
@@ -3829,9 +3835,9 @@ hipError_t launch_sph_materialize(const SphBuffers& b, const f4* st, const uint3
   hipLaunchKernelGGL(sph_materialize_kernel, dim3(blocks_for(slots)), dim3(kBlock), 0, s, st, perm, dst, b.sl, slots);
   return hipGetLastError();
 }
-hipError_t launch_sph_pad_unflag(const SphBuffers& b, hipStream_t s) {
-  if (b.p == b.n) return hipSuccess;
-  hipLaunchKernelGGL(sph_pad_unflag_kernel, dim3(blocks_for(b.p - b.n)), dim3(kBlock), 0, s, b.lookup, b.n, b.p);
+hipError_t launch_sph_lookup_canonical(const SphBuffers& b, const uint32_t* perm, hipStream_t s) {
+  if (b.p == b.n && !perm) return hipSuccess;
+  hipLaunchKernelGGL(sph_lookup_canonical_kernel, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.lookup, perm, b.p);
   return hipGetLastError();
 }
 hipError_t launch_sph_lookup_translate(const uint2* lookup, const uint32_t* perm, uint2* out, uint32_t p,

@@ -167,6 +167,7 @@ _P = ctypes.c_void_p
 _U32, _U64, _I = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
 ABI_SYMBOLS = [
     ("rps_abi_version", _U32, []),
+    ("rps_build_id", ctypes.c_char_p, []),
     ("rps_status_string", ctypes.c_char_p, [_I]),
     ("rps_device_count", _I, [ctypes.POINTER(_I)]),
     ("rps_create", _I, [ctypes.POINTER(CreateInfo), ctypes.POINTER(_P)]),
@@ -216,6 +217,28 @@ def lib() -> ctypes.CDLL:
         fn.argtypes = args
     _lib = L
     return L
+
+
+# The sources librps.so is built from, in the Makefile's order (SRCS, then HDRS): their sha256
+# is the library's rps_build_id() when it was built from this tree.
+_BUILD_SOURCES = ("csrc/rps_kernels.hip", "csrc/rps_nbody.hip", "csrc/rps_context.hip",
+                  "csrc/rps_device.hpp", "csrc/rps_internal.hpp", "../include/rps.h")
+
+
+def source_build_id() -> str:
+    """sha256 (16 hex digits) of this tree's librps sources, as the Makefile's BUILD_ID."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for rel in _BUILD_SOURCES:
+        with open(os.path.normpath(os.path.join(PKG_ROOT, rel)), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def build_id() -> str:
+    """The loaded library's build id (rps_build_id)."""
+    return lib().rps_build_id().decode()
 
 
 def device_count() -> int:

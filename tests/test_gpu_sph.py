@@ -188,6 +188,9 @@ def test_sph_resident_state_api(gpu, orc, monkeypatch, n):
         ctx.step(2)
         frames(2)
         assert_soa_bitwise(ctx.download_soa(), ref, what="after export ")
+        # the lookup right after the download (which puts the state back in particle order):
+        # the reference's spatial_lookup, pads included (particle indices, not slots)
+        assert_bitwise(ctx.read_debug(rps.DEBUG_SPATIAL_LOOKUP), st.lookup, "lookup after download")
         ctx.step(2)
         frames(2)
         x_new = (ref["x"][:100] * np.float32(0.5)).astype(F)
@@ -535,16 +538,8 @@ def test_sph_spatial_layout_gated_frames(gpu, orc, monkeypatch):
             assert_soa_bitwise(ctx.download_soa(), ref, what=f"f{frame} ")
 
 
-def test_sph_layout_clustered_runs(gpu, orc, monkeypatch):
-    """Runs longer than the layout's 32-entry measure (a clump of particles in one cell) are
-    'listed' by the runs kernel.  Their lengths come from the per-key run ends and their slots'
-    prediction is spread over every thread of the write kernel (round 2 walked and predicted
-    each listed run on one lane, O(run length) dependent loads).  At 2^21 (a default layout
-    size) with 16 clumps of 4096 particles each inside one cell: the first frame bitwise
-    against the oracle, with and without the layout.  (The timing comparison of the two record
-    placements on this state lives in tools/ab_sph.py, not in this correctness suite.)"""
-    rps = gpu
-    n = 1 << 21
+def _clumped_state(rps, n):
+    """The reference scatter at 2^21 with 16 clumps of 4096 particles inside one cell each."""
     scale = (n / 50000) ** 0.5
     cfg = rps.default_particle_config(n, screen_bounds=rps.screen_bounds_for(1920.0 * scale, 1080.0 * scale))
     parts = rps.setup_particles_scatter(cfg, n, seed=0x5EED)
@@ -560,6 +555,19 @@ def test_sph_layout_clustered_runs(gpu, orc, monkeypatch):
         sl = slice(c * k, (c + 1) * k)
         soa["x"][sl] = (cx + g.uniform(-0.2 * r, 0.2 * r, k)).astype(F)
         soa["y"][sl] = (cy + g.uniform(-0.2 * r, 0.2 * r, k)).astype(F)
+    return cfg, soa
+
+
+def test_sph_layout_clustered_runs(gpu, orc, monkeypatch):
+    """Runs longer than the layout's 32-entry measure (a clump of particles in one cell) are
+    'listed' by the runs kernel.  Their lengths come from the per-key run ends and their slots'
+    prediction is spread over every thread of the write kernel (round 2 walked and predicted
+    each listed run on one lane, O(run length) dependent loads).  At 2^21 (a default layout
+    size) with 16 clumps of 4096 particles each inside one cell: the first frame bitwise
+    against the oracle, with and without the layout (timing: the next test)."""
+    rps = gpu
+    n = 1 << 21
+    cfg, soa = _clumped_state(rps, n)
     ext = rps.make_ext(shader_delay=0)
     st = orc.SphState(n, omp=True)
     ref = copy_soa(soa)
@@ -643,3 +651,22 @@ def test_sph_particle_order_bin_entries(gpu, orc, n):
         assert_bitwise(ctx.read_debug(rps.DEBUG_SPATIAL_LOOKUP), st.lookup, "lookup after config change")
         assert_bitwise(ctx.read_debug(rps.DEBUG_LOOKUP_OFFSETS), st.offsets, "offsets after config change")
         assert_soa_bitwise(ctx.download_soa(), ref, what="after config change ")
+
+
+def test_sph_layout_clustered_runs_timing(gpu, monkeypatch):
+    """Performance regression bound on the listed-run path: on the clumped 2^21 state a frame
+    with the spatial layout costs at most 3x a lookup-order frame (measured ~1x,
+    tools/ab_sph.py; round 2's per-lane walk of listed runs was many times slower)."""
+    rps = gpu
+    n = 1 << 21
+    cfg, soa = _clumped_state(rps, n)
+    ms = {}
+    for layout in ("1", "0"):
+        monkeypatch.setenv("RPS_SPH_LAYOUT", layout)
+        with rps.Context(n, rps.MODE_SPH) as ctx:
+            ctx.set_config(cfg, rps.make_ext(shader_delay=0))
+            ctx.upload_soa(soa)
+            ctx.step(3)
+            ctx.sync()
+            ms[layout] = ctx.time_steps(10) / 10
+    assert ms["1"] <= 3.0 * ms["0"], ms

@@ -5,7 +5,7 @@
 set -euo pipefail
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 name=$1; src=$2; shift 2
-out=$ROOT/ablibs/$name
+out=${AB_OUT:-$ROOT/ablibs}/$name
 mkdir -p "$out"
 cp "$src" "$ROOT/rust-particle-system_amd/csrc/.variant_$name.hip"
 cp "${CTX_SRC:-$ROOT/rust-particle-system_amd/csrc/rps_context.hip}" "$ROOT/rust-particle-system_amd/csrc/.variant_ctx_$name.hip"

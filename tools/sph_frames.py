@@ -10,6 +10,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "rust-particle-system_amd", "python"))
 import rps_amd as rps  # noqa: E402
 
+if os.environ.get("AB_LIB"):  # a variant build (tools/build_variant.sh) for A/B traces
+    rps.LIB_PATH = os.path.abspath(os.environ["AB_LIB"])
+
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 50000
 frames = int(sys.argv[2]) if len(sys.argv) > 2 else 50
 warm = int(sys.argv[3]) if len(sys.argv) > 3 else 10
