@@ -123,6 +123,92 @@ def tail(tile, TLOG):
     return v.reshape(-1, 2)
 
 
+def xstrides(v, t, LG):
+    """xlane_strides<LG>: strides 2^LG .. 32 as lane exchanges (lane t ^ 2^(LG-3) .. t ^ 4)."""
+    while LG >= 5:
+        D = 1 << (LG - 3)
+        xlane(v, t ^ D, False, (t & D) == 0)
+        LG -= 1
+    return v
+
+
+def reg_tail_x(v, t):
+    """reg_tail<true>: strides 16 (xor-2 lanes), 8 (xor-1 lanes), then 4, 2, 1 in-lane."""
+    xlane(v, t ^ 2, False, (t & 2) == 0)
+    xlane(v, t ^ 1, False, (t & 1) == 0)
+    group_passes(v, 3)
+
+
+def mid_chunks_x(lds, nt, LG):
+    """lds_mid_chunks_x<LG>: three-pass LDS chunks while the chunk's top stride is >= 512 entries;
+    returns the top stride left for the lane exchanges (lds_mid_rem)."""
+    while LG >= 9:
+        lds_chunk(lds, nt, LG, 3)
+        LG -= 3
+    return LG
+
+
+def tail_x(tile, TLOG):
+    """The round-5 cross-lane tail (measured slower; the kernels run `tail`):
+    strides TILE/2 .. TILE/8 on strided entries, LDS chunks for the strides that cross waves, the
+    rest on each lane's eight consecutive entries by lane exchanges."""
+    nt = 1 << (TLOG - 3)
+    t = np.arange(nt)
+    v = tile[t[:, None] + np.arange(8)[None, :] * nt].copy()
+    group_passes(v, 3)
+    lds = np.zeros_like(tile)
+    lds[t[:, None] + np.arange(8)[None, :] * nt] = v
+    LG = mid_chunks_x(lds, nt, TLOG - 4)
+    v = lds[8 * t[:, None] + np.arange(8)[None, :]].copy()
+    xstrides(v, t, LG)
+    reg_tail_x(v, t)
+    return v.reshape(-1, 2)
+
+
+def head_x(tile, TLOG):
+    """The round-5 cross-lane head (measured slower; the kernels run `head`):
+    stages
+    5 .. 8 (spans up to 512 = one wave) entirely by lane exchanges (the flip with the mirror lane,
+    entries reversed), later stages' flip and cross-wave strides in LDS, the rest by lanes."""
+    nt = 1 << (TLOG - 3)
+    t = np.arange(nt)
+    v = tile.reshape(nt, 8, 2).copy()
+    for pairs in ([(0, 1), (2, 3), (4, 5), (6, 7)], [(0, 3), (1, 2), (4, 7), (5, 6)],  # reg_stages012
+                  [(0, 1), (2, 3), (4, 5), (6, 7)], [(0, 7), (1, 6), (2, 5), (3, 4)],
+                  [(0, 2), (1, 3), (4, 6), (5, 7)], [(0, 1), (2, 3), (4, 5), (6, 7)]):
+        for i, j in pairs:
+            cas(v, i, j)
+    xlane(v, t ^ 1, True, (t & 1) == 0)  # stage 3
+    group_passes(v, 3)
+    xlane(v, t ^ 3, True, (t & 2) == 0)  # stage 4
+    xlane(v, t ^ 1, False, (t & 1) == 0)
+    group_passes(v, 3)
+    lds = np.zeros_like(tile)
+    own = 8 * t[:, None] + np.arange(8)[None, :]
+    for S in range(5, TLOG):
+        if S <= 8:
+            M = 1 << (S - 2)  # lanes per flip block
+            xlane(v, t ^ (M - 1), True, (t & (M // 2)) == 0)
+            xstrides(v, t, S - 1)
+        else:
+            lds[own] = v
+            g = 1 << (S - 1)
+            LP = S - 2
+            base = (t >> LP) << (S + 1)
+            r = t & ((1 << LP) - 1)
+            ia = base[:, None] + r[:, None] + np.arange(4)[None, :] * g
+            ib = base[:, None] + (g - 1 - r)[:, None] + np.arange(4)[None, :] * g
+            w = np.concatenate([lds[ia], lds[ib]], 1)
+            for i, j in ((0, 7), (1, 6), (4, 3), (5, 2), (0, 1), (2, 3), (4, 5), (6, 7)):  # lds_flip_chunk
+                cas(w, i, j)
+            lds[ia], lds[ib] = w[:, :4], w[:, 4:]
+            LG = mid_chunks_x(lds, nt, S - 2)
+            v = lds[own].copy()
+            xstrides(v, t, LG)
+        reg_tail_x(v, t)
+    return v.reshape(-1, 2)
+
+
 def lane_stage(v, S):
     B = 1 << (S + 1)
     for b in range(0, 16, B):
@@ -263,18 +349,20 @@ def test_store_eight_writes_each_lane_to_its_entries():
 
 @pytest.mark.parametrize("TLOG", [11, 12, 13])
 @pytest.mark.parametrize("kmax", [7, 1 << 20])
-@pytest.mark.parametrize("layout", ["eight", "sixteen"])
+@pytest.mark.parametrize("layout", ["cross-lane", "eight", "sixteen"])
 def test_head_schedule_equals_network(TLOG, kmax, layout):
+    """eight: the kernels' schedule (every stage from 5 on through LDS); cross-lane (round 5) and
+    sixteen (round 3): measured-slower alternatives, kept replayed."""
     g = np.random.default_rng(TLOG * 7 + (kmax & 3))
     keys = g.integers(0, kmax, 1 << TLOG)  # kmax 7: dense ties; 2^20: mostly distinct
     tile = np.stack([keys, np.arange(len(keys))], 1).astype(np.int64)
-    run = head if layout == "eight" else head16
+    run = {"cross-lane": head_x, "eight": head, "sixteen": head16}[layout]
     np.testing.assert_array_equal(run(tile, TLOG), ref_network(keys, TLOG))
 
 
 @pytest.mark.parametrize("TLOG", [11, 12, 13])
 @pytest.mark.parametrize("kmax", [7, 1 << 20])
-@pytest.mark.parametrize("layout", ["eight", "sixteen"])
+@pytest.mark.parametrize("layout", ["cross-lane", "eight", "sixteen"])
 def test_tail_schedule_equals_network(TLOG, kmax, layout):
     """A later stage s's passes inside one tile: strides 2^(TLOG-1) .. 1, non-flip (the tile
     after the stage's global passes; any input order)."""
@@ -294,7 +382,7 @@ def test_tail_schedule_equals_network(TLOG, kmax, layout):
         sw = a[left, 0] > a[right, 0]
         l, r = a[left[sw]].copy(), a[right[sw]].copy()
         a[left[sw]], a[right[sw]] = r, l
-    np.testing.assert_array_equal((tail if layout == "eight" else tail16)(tile, TLOG), a)
+    np.testing.assert_array_equal({"cross-lane": tail_x, "eight": tail, "sixteen": tail16}[layout](tile, TLOG), a)
 
 
 def test_store_sixteen_places_each_lane_contiguously():
