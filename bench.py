@@ -364,6 +364,54 @@ def configs_side(rps, args, d):
     return out
 
 
+def sph_roofline(cost, sim_ms, frame_ms, pmc):
+    """The SPH line's `roofline` and `frame_cost` objects.  Measured traffic (PMC, the bench
+    workload at 2^22; profiles/pmc_traffic.json): the sim kernel's L1 -> L2 request bytes and
+    memory-side bytes per launch, and every SPH kernel's memory-side bytes per frame.  `frac` is a
+    utilisation: the measured L1 -> L2 bytes' rate against the aggregate L2 peak (the scans'
+    gathers are mostly L1 hits, so the algorithmic bytes -- every neighbour gather charged -- only
+    give an equivalence rate, `algorithmic_equiv_*`).  Without a PMC record the rates are null."""
+    pmc_src = f"profiles/pmc_traffic.json 'SPH-2^22-frame' (round {pmc.get('round')}; not this run)" if pmc else None
+    sim_name, sim_pmc = next(((k, v) for k, v in (pmc or {}).get("per_dispatch", {}).items()
+                              if k.startswith("sph_sim")), (None, None))
+    sim_l2 = sim_pmc["l2_read_bytes"] + sim_pmc["l2_write_bytes"] if sim_pmc else None
+    sim_hbm = sim_pmc.get("hbm_bytes") if sim_pmc else None
+
+    def rate(b, ms):
+        return b / (ms * 1e-3) / 1e9 if b else None
+
+    def frac(b, ms, peak):
+        return rate(b, ms) / peak if b else None
+
+    hbm_frame = (pmc or {}).get("frame_sum_of_kernels", {}).get("hbm_bytes")
+    l2_frame = (pmc or {}).get("frame_sum_of_kernels", {}).get("l2_bytes")
+    sim_algo_gbps = cost["sim_bytes"] / (sim_ms * 1e-3) / 1e9
+    roofline = {"bound": "l2", "kernel": sim_name or "sph_sim_kernel",
+                "achieved": rate(sim_l2, sim_ms), "peak": L2_PEAK_GBPS, "unit": "GB/s",
+                "frac": frac(sim_l2, sim_ms, L2_PEAK_GBPS), "traffic": sim_l2,
+                "hbm_bytes_per_launch": sim_hbm, "hbm_gbps": rate(sim_hbm, sim_ms),
+                "hbm_frac": frac(sim_hbm, sim_ms, HBM_PEAK_GBPS),
+                "traffic_source": pmc_src,
+                "algorithmic_bytes_per_launch": cost["sim_bytes"],
+                "algorithmic_equiv_gbps": sim_algo_gbps,
+                "algorithmic_equiv_frac": sim_algo_gbps / L2_PEAK_GBPS,
+                "scanned_entries_per_particle": cost["scanned_entries"] / cost["slots"],
+                "within_radius_per_particle": cost["within_entries"] / cost["slots"],
+                "note": "achieved/frac: the sim kernel's L1 -> L2 request bytes measured by the PMC counters "
+                        "(traffic, per launch) / this run's kernel time, against the aggregate L2 peak; "
+                        "hbm_frac: its memory-side bytes against HBM; algorithmic_equiv_*: every neighbour "
+                        "gather charged (mostly L1 hits) -- an equivalence, not a utilisation"}
+    frame_cost = {"hbm_bytes_measured": hbm_frame, "hbm_bytes_source": pmc_src,
+                  "hbm_gbps": rate(hbm_frame, frame_ms), "frac": frac(hbm_frame, frame_ms, HBM_PEAK_GBPS),
+                  "bound": "hbm", "peak": HBM_PEAK_GBPS,
+                  "l2_bytes_measured": l2_frame, "l2_frac": frac(l2_frame, frame_ms, L2_PEAK_GBPS),
+                  "algorithmic_bytes": cost["frame_bytes"],
+                  "algorithmic_equiv_frac_of_l2": cost["frame_bytes"] / (frame_ms * 1e-3) / 1e9 / L2_PEAK_GBPS,
+                  "sort_launches": cost["sort_launches"],
+                  "note": "frac: the frame's memory-side bytes (sum over its kernels, PMC) per frame time against HBM"}
+    return roofline, frame_cost
+
+
 def sph_side(rps, args, d):
     """Side measurement: the reference's full five-pass SPH frame (bin,
     bitonic sort, offsets, pre-simulation, simulation) at `sph_n` particles, the reference
@@ -396,22 +444,8 @@ def sph_side(rps, args, d):
         ctx.close()
     sim_ms = d.max(sim_ms)
     frame_ms = el * 1e3 / args.sph_frames
-    sim_algo_gbps = cost["sim_bytes"] / (sim_ms * 1e-3) / 1e9
-    # Measured traffic (PMC, the bench workload at 2^22; profiles/pmc_traffic.json): the sim
-    # kernel's L1 -> L2 request bytes and memory-side bytes per launch, and every SPH kernel's
-    # memory-side bytes per frame.  `frac` is a utilisation: the measured L1 -> L2 bytes' rate
-    # against the aggregate L2 peak (the scans' gathers are mostly L1 hits, so the algorithmic
-    # bytes -- every neighbour gather charged -- only give an equivalence rate).
     pmc = pmc_sph() if n == 1 << 22 else None
-    pmc_src = f"profiles/pmc_traffic.json 'SPH-2^22-frame' (round {pmc.get('round')}; not this run)" if pmc else None
-    sim_name, sim_pmc = next(((k, v) for k, v in (pmc or {}).get("per_dispatch", {}).items()
-                              if k.startswith("sph_sim")), (None, None))
-    sim_l2 = sim_pmc["l2_read_bytes"] + sim_pmc["l2_write_bytes"] if sim_pmc else None
-    sim_hbm = sim_pmc.get("hbm_bytes") if sim_pmc else None
-    rate = lambda b, ms: b / (ms * 1e-3) / 1e9 if b else None  # noqa: E731
-    frac = lambda b, ms, peak: rate(b, ms) / peak if b else None  # noqa: E731
-    hbm_frame = (pmc or {}).get("frame_sum_of_kernels", {}).get("hbm_bytes")
-    l2_frame = (pmc or {}).get("frame_sum_of_kernels", {}).get("l2_bytes")
+    rl, fc = sph_roofline(cost, sim_ms, frame_ms, pmc)
     slots = 1 << max(0, (n - 1).bit_length())  # P = next_pow2(N) (particle_buffers.rs:86)
     layout = os.environ.get("RPS_SPH_LAYOUT", "1")
     spatial = layout == "2" or (layout == "1" and slots >= (1 << 20))  # rps_context.hip
@@ -419,31 +453,7 @@ def sph_side(rps, args, d):
            "record_layout": "cell tiles (spatial)" if spatial else "lookup order",
            "scaling": "replicas", "frames": args.sph_frames, "ms_per_frame": frame_ms,
            "particle_steps_per_s": float(n) * d.world * args.sph_frames / el,
-           "sim_kernel_ms": sim_ms,
-           "roofline": {"bound": "l2", "kernel": sim_name or "sph_sim_kernel",
-                        "achieved": rate(sim_l2, sim_ms), "peak": L2_PEAK_GBPS, "unit": "GB/s",
-                        "frac": frac(sim_l2, sim_ms, L2_PEAK_GBPS), "traffic": sim_l2,
-                        "hbm_bytes_per_launch": sim_hbm, "hbm_gbps": rate(sim_hbm, sim_ms),
-                        "hbm_frac": frac(sim_hbm, sim_ms, HBM_PEAK_GBPS),
-                        "traffic_source": pmc_src,
-                        "algorithmic_bytes_per_launch": cost["sim_bytes"],
-                        "algorithmic_equiv_gbps": sim_algo_gbps,
-                        "algorithmic_equiv_frac": sim_algo_gbps / L2_PEAK_GBPS,
-                        "scanned_entries_per_particle": cost["scanned_entries"] / cost["slots"],
-                        "within_radius_per_particle": cost["within_entries"] / cost["slots"],
-                        "note": "achieved/frac: the sim kernel's L1 -> L2 request bytes measured by the PMC "
-                                "counters (traffic, per launch) / this run's kernel time, against the aggregate "
-                                "L2 peak; hbm_frac: its memory-side bytes against HBM; algorithmic_equiv_*: every "
-                                "neighbour gather charged (mostly L1 hits) -- an equivalence, not a utilisation"},
-           "frame_cost": {"hbm_bytes_measured": hbm_frame, "hbm_bytes_source": pmc_src,
-                          "hbm_gbps": rate(hbm_frame, frame_ms), "frac": frac(hbm_frame, frame_ms, HBM_PEAK_GBPS),
-                          "bound": "hbm", "peak": HBM_PEAK_GBPS,
-                          "l2_bytes_measured": l2_frame, "l2_frac": frac(l2_frame, frame_ms, L2_PEAK_GBPS),
-                          "algorithmic_bytes": cost["frame_bytes"],
-                          "algorithmic_equiv_frac_of_l2": cost["frame_bytes"] / (frame_ms * 1e-3) / 1e9 / L2_PEAK_GBPS,
-                          "sort_launches": cost["sort_launches"],
-                          "note": "frac: the frame's memory-side bytes (sum over its kernels, PMC) per frame time "
-                                  "against HBM"}}
+           "sim_kernel_ms": sim_ms, "roofline": rl, "frame_cost": fc}
     out["reference_sizes"] = [sph_small(rps, args, d, m) for m in (50000, 65536)]
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline and args.sph_cpu_n > 0:
         out["cpu_baseline"] = sph_cpu_baseline(rps, args)
