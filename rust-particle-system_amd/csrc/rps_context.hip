@@ -512,7 +512,15 @@ int sph_frame_begin(rps_ctx* ctx, bool layout) {
 
 int step_sph_sim(rps_ctx* ctx, bool layout, const SphGrid& g) {
   ctx->layout_last = layout;
-  if (layout) ctx->lay.g = g;
+  if (layout) {
+    ctx->lay.g = g;
+    // cell_info records carry the build's epoch (the arena's zeros are epoch 0); at the wrap the
+    // old records are cleared so none can match a reused epoch
+    if (++ctx->lay.epoch >= (1u << 24)) {
+      RPS_HIP(ctx, hipMemsetAsync(ctx->lay.cell_info, 0, (size_t)ctx->cell_cap * 2 * sizeof(uint4), ctx->stream));
+      ctx->lay.epoch = 1;
+    }
+  }
   ++ctx->sl.owner_epoch;  // this active frame's owner claims (SphSlots::owner)
   SphBuffers b = sph_buffers(ctx);
   if (layout)
@@ -747,6 +755,8 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     set_sph_fields(ctx);
     // A layout frame does not run pass 3, so its run ends go to the key-indexed ends array.
     if (ctx->cell_cap) ctx->lay.run_end = ctx->ends;
+    // test hook: the epoch the layout builds count from (the wrap at 2^24, step_sph_sim)
+    ctx->lay.epoch = (uint32_t)std::clamp(env_int("RPS_SPH_LAYOUT_EPOCH", 0), 0, (1 << 24) - 1);
   }
   if (ctx->mode == RPS_MODE_STREAM) {
     ctx->layout = tiled_layout();

@@ -138,8 +138,9 @@ struct SphGrid {
 };
 struct SphLayoutArgs {
   SphGrid g;
-  uint4* cell_info;    // 2 x cells: {first slot, length, 6 particle indices} of the run a cell
-                       //   owns (length 0: none)
+  uint4* cell_info;    // 2 x cells: {first slot, length | epoch << 8, 6 particle indices} of the
+                       //   run a cell owns (another epoch: none; so it is never reset)
+  uint32_t epoch;      // this layout build's (1 ... 2^24 - 1; cell_info cleared at the wrap)
   uint2* cellrun;      // cells: storage {start, end} of the cell's key's run (start >= N: none)
   uint2* run2;         // N: storage {start, end} per key ({0xFFFFFFFF, 0}: none; reset in bin)
   uint32_t* part;      // cells / 256 + 2: 256-cell block sums -> bases; [blocks]: the grid's

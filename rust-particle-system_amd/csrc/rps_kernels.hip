@@ -2973,8 +2973,9 @@ __global__ __launch_bounds__(kBlock) void sph_count_kernel(const rps_config* __r
 // cells sit next to each other, and a cell-ordered table of storage runs (cellrun) replaces
 // the scans' key-indexed (hash-random) run bounds:
 //   runs kernel (slot order, in place of pass 3): at a run start, the run's length and the
-//       cell of its first particle (its owner): cell_info[cell] = {first slot, length, the
-//       first kRunIdx particle indices}; runs whose first particle lies outside the grid (or
+//       cell of its first particle (its owner): cell_info[cell] = {first slot, length tagged
+//       with the build's epoch (a stale record needs no reset pass), the first kRunIdx particle
+//       indices}; runs whose first particle lies outside the grid (or
 //       longer than kRunScan) go to a list (the reference's offsets are rebuilt on readback);
 //   block counts (256 cells) and one-workgroup scan: block bases; listed runs after the grid's;
 //   write (cell order): each owned run gets the next storage range -> run2[key], cellrun[cell];
@@ -3070,15 +3071,20 @@ __global__ __launch_bounds__(kBlock) void sph_runs_kernel(SphLayoutArgs a, const
   if (c == kCellOut || len > kRunScan) {
     a.out_runs[atomicAdd(a.n_out, 1u)] = make_uint2(t, 0u);  // placed by the scan kernel
   } else {
-    a.cell_info[2u * c] = make_uint4(t, len, idx[0], idx[1]);
+    a.cell_info[2u * c] = make_uint4(t, len | a.epoch << 8, idx[0], idx[1]);
     a.cell_info[2u * c + 1u] = make_uint4(idx[2], idx[3], idx[4], idx[5]);
   }
+}
+
+// The length of the run cell e owns this frame (0: none; a record of another epoch is stale).
+__device__ __forceinline__ uint32_t owned_len(const SphLayoutArgs& a, uint32_t v) {
+  return v >> 8 == a.epoch ? v & 0xFFu : 0u;
 }
 
 // Run lengths owned by each 256-cell block.
 __global__ __launch_bounds__(kBlock) void sph_layout_count_kernel(SphLayoutArgs a) {
   const uint32_t e = blockIdx.x * kBlock + threadIdx.x;
-  const uint32_t len = e < a.g.cells ? a.cell_info[2u * e].y : 0u;
+  const uint32_t len = owned_len(a, e < a.g.cells ? a.cell_info[2u * e].y : 0u);
   uint32_t tot;
   block_exclusive_scan<kBlock>(len, &tot);
   if (threadIdx.x == 0) a.part[blockIdx.x] = tot;
@@ -3144,7 +3150,7 @@ __global__ __launch_bounds__(kBlock) void sph_layout_write_kernel(SphLayoutArgs 
   const bool in = e < a.g.cells;
   const uint4 i0 = in ? a.cell_info[2u * e] : make_uint4(0u, 0u, 0u, 0u);
   const uint4 i1 = in ? a.cell_info[2u * e + 1u] : make_uint4(0u, 0u, 0u, 0u);
-  const uint32_t len = i0.y;
+  const uint32_t len = owned_len(a, i0.y);
   const uint32_t b0 = a.part[blockIdx.x];
   uint32_t tot;
   const uint32_t rel = block_exclusive_scan<kBlock>(len, &tot);
@@ -3159,7 +3165,6 @@ __global__ __launch_bounds__(kBlock) void sph_layout_write_kernel(SphLayoutArgs 
   for (uint32_t r = 0; r < len && rel + r < kSlotMap; ++r) lcell[rel + r] = (uint8_t)threadIdx.x;
   if (in) {
     if (len) {
-      a.cell_info[2u * e] = make_uint4(0u, 0u, 0u, 0u);  // empty again for the next frame
       int32_t cx, cy;
       grid_cell(a.g, e, cx, cy);  // the owner's key is its cell's key (sph_runs_kernel)
       const uint2 run = make_uint2(b0 + rel, b0 + rel + len);

@@ -153,6 +153,18 @@ def test_sph_resident_state_frames(gpu, orc, monkeypatch, n):
                       download_at={3, 6})
 
 
+def test_sph_layout_epoch_wrap(gpu, orc, monkeypatch):
+    """The layout's cell records carry the build's epoch instead of being reset each frame;
+    started two builds before the 2^24 wrap, the frames across it (records cleared, epoch 1
+    again) stay bitwise."""
+    rps = gpu
+    monkeypatch.setenv("RPS_SPH_LAYOUT", "2")
+    monkeypatch.setenv("RPS_SPH_LAYOUT_EPOCH", str((1 << 24) - 3))
+    n = 16384
+    cfg = rps.default_particle_config(n, gravity=100.0)
+    _frames_vs_oracle(rps, orc, n, _blob(n, 47, spread=300.0), cfg, 5, download_at={4})
+
+
 @pytest.mark.parametrize("n", [16384, 16000])
 def test_sph_resident_state_api(gpu, orc, monkeypatch, n):
     """Every particle-order API call on slot-resident state: a device export, a partial field
