@@ -514,10 +514,11 @@ int step_sph_sim(rps_ctx* ctx, bool layout, const SphGrid& g) {
   ctx->layout_last = layout;
   if (layout) {
     ctx->lay.g = g;
-    // cell_info records carry the build's epoch (the arena's zeros are epoch 0); at the wrap the
-    // old records are cleared so none can match a reused epoch
+    // cell_info and key_cell records carry the build's epoch (the arena's zeros are epoch 0); at
+    // the wrap the old records are cleared so none can match a reused epoch
     if (++ctx->lay.epoch >= (1u << 24)) {
       RPS_HIP(ctx, hipMemsetAsync(ctx->lay.cell_info, 0, (size_t)ctx->cell_cap * 2 * sizeof(uint4), ctx->stream));
+      RPS_HIP(ctx, hipMemsetAsync(ctx->lay.key_cell, 0, (size_t)ctx->n * sizeof(uint2), ctx->stream));
       ctx->lay.epoch = 1;
     }
   }
@@ -714,6 +715,7 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
       slots.push_back({(void**)&ctx->lay.run2, align_up(n * sizeof(uint2), 256)});
       slots.push_back({(void**)&ctx->lay.part, align_up((cap / 256 + 2) * sizeof(uint32_t), 256)});
       slots.push_back({(void**)&ctx->lay.out_runs, align_up(n * sizeof(uint2), 256)});
+      slots.push_back({(void**)&ctx->lay.key_cell, align_up(n * sizeof(uint2), 256)});
       slots.push_back({(void**)&ctx->lay.keybits, align_up((n / 32 + 1) * sizeof(uint32_t), 256)});
       slots.push_back({(void**)&ctx->lay.n_out, 256});
       // slot-resident state: the buffer st swaps with, the previous slot -> particle map, the

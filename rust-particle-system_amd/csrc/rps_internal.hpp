@@ -140,9 +140,11 @@ struct SphLayoutArgs {
   SphGrid g;
   uint4* cell_info;    // 2 x cells: {first slot, length | epoch << 8, 6 particle indices} of the
                        //   run a cell owns (another epoch: none; so it is never reset)
-  uint32_t epoch;      // this layout build's (1 ... 2^24 - 1; cell_info cleared at the wrap)
+  uint32_t epoch;      // this layout build's (1 ... 2^24 - 1; cell_info, key_cell cleared at the wrap)
   uint2* cellrun;      // cells: storage {start, end} of the cell's key's run (start >= N: none)
-  uint2* run2;         // N: storage {start, end} per key ({0xFFFFFFFF, 0}: none; reset in bin)
+  uint2* run2;         // N: storage {start, end} of the listed runs, by key (never reset)
+  uint2* key_cell;     // N: {owner cell, or kCellOut for a listed run; epoch} of each key's run
+                       //   (another epoch: the key has no run this build)
   uint32_t* part;      // cells / 256 + 2: 256-cell block sums -> bases; [blocks]: the grid's
                        //   total (the listed runs' storage starts there)
   uint2* out_runs;     // N: {first slot, storage base} of the runs placed after the grid's

@@ -659,9 +659,8 @@ struct SortBin {
   const f4* st;  // packed {x, y, vx, vy} per particle
   uint32_t* offsets;
   uint32_t n;
-  uint2* run2;  // spatial layout's storage runs, reset with offsets (nullptr: no layout)
   const uint2* prebuilt;  // bin entries the previous frame's sim wrote (nullptr: from positions)
-  bool reset_pre;         // prebuilt entries in particle order (no layout): still reset offsets/run2
+  bool reset_pre;         // prebuilt entries in particle order (no layout): still reset offsets
 };
 
 __device__ __forceinline__ f2 bin_pos(const SortBin& b, uint32_t i) {
@@ -669,7 +668,6 @@ __device__ __forceinline__ f2 bin_pos(const SortBin& b, uint32_t i) {
 }
 __device__ __forceinline__ void bin_reset(const SortBin& b, uint32_t i) {
   b.offsets[i] = 0xFFFFFFFFu;
-  if (b.run2) b.run2[i] = make_uint2(0xFFFFFFFFu, 0u);
 }
 __device__ __forceinline__ uint2 bin_key(const SortBin& b, f2 pos, uint32_t i) {
   bin_reset(b, i);
@@ -1232,8 +1230,8 @@ __device__ __forceinline__ void head_stages(uint2* lds, uint32_t t, uint2 (&v)[8
   }
 }
 
-// The bin pass's inputs for a tile (entries q = t + k*NT: a wave's loads and its offsets / run2
-// resets cover consecutive particles): positions, or the previous frame's pad entries [n, P)
+// The bin pass's inputs for a tile (entries q = t + k*NT: a wave's loads and its offsets resets
+// cover consecutive particles): positions, or the previous frame's pad entries [n, P)
 // (the reference never rewrites them).
 template <uint32_t NT>
 __device__ __forceinline__ void bin_load(const uint2* lookup, const SortBin& bin, uint32_t base0, uint32_t t,
@@ -1252,9 +1250,9 @@ __device__ __forceinline__ void bin_keys(const SortBin& bin, uint32_t base0, uin
     const uint32_t q = t + k * NT, gq = base0 + q;
     if (gq >= bin.n) {
       s[q] = raw[k];
-    } else if (bin.prebuilt) {  // (key, slot) of a layout frame: run2 is reset by the runs kernel,
-      if (bin.reset_pre) bin_reset(bin, gq);  // offsets on debug readback (rps_read_debug); the
-      s[q] = raw[k];                           // sim's (key, i) of a frame without layout: both
+    } else if (bin.prebuilt) {  // (key, slot) of a layout frame: offsets are rebuilt on debug
+      if (bin.reset_pre) bin_reset(bin, gq);  // readback (rps_read_debug); the sim's (key, i) of a
+      s[q] = raw[k];                           // frame without layout: reset here
     } else {
       s[q] = bin_key(bin, __builtin_bit_cast(f2, raw[k]), gq);
     }
@@ -1741,7 +1739,7 @@ __global__ __launch_bounds__(kBlock) void sph_offsets_kernel(const uint2* __rest
 // Spatial record layout: cell enumeration (8 x 8 tiles; see the layout kernels below; tall
 // tiles measured equal).
 constexpr uint32_t kCellOut = 0xFFFFFFFFu;
-constexpr uint32_t kCellPending = 0xFFFFFFFEu;  // cellrun entry to resolve through run2
+constexpr uint32_t kCellPending = 0xFFFFFFFEu;  // cellrun entry the fixup resolves by key
 constexpr uint32_t kRunScan = 32u;               // longest run a runs-kernel lane measures itself
 constexpr uint32_t kRunIdx = 6u;                 // particle indices a run's cell_info records
 
@@ -1895,16 +1893,27 @@ __device__ __forceinline__ uint32_t grid_key(int32_t cx, int32_t cy, int o, uint
 }
 
 // Where a scan finds the run of a neighbour cell: key-indexed {offsets, ends} in lookup order,
-// or (spatial layout) the cell-ordered storage runs, with the key-indexed run2 for lanes whose
+// or (spatial layout) the cell-ordered storage runs, found by key (key_run) for lanes whose
 // 3 x 3 block leaves the layout's grid.
 struct RunBounds {
   const uint32_t* offsets;
   const uint32_t* ends;
   const uint2* cellrun;
   const uint2* run2;
+  const uint2* key_cell;
+  uint32_t epoch;
   SphGrid g;
   uint32_t* keybits;  // SphLayoutArgs::keybits (the density pass clears it for the next frame)
 };
+
+// The storage run of key k in a layout frame: its owner cell's (cellrun), or a listed run's
+// (run2); none ({0xFFFFFFFF, 0}) if the key has no run this build (key_cell of another epoch).
+__device__ __forceinline__ uint2 key_run(const uint2* __restrict__ key_cell, const uint2* __restrict__ cellrun,
+                                         const uint2* __restrict__ run2, uint32_t epoch, uint32_t k) {
+  const uint2 kc = key_cell[k];
+  if (kc.y != epoch) return make_uint2(0xFFFFFFFFu, 0u);
+  return kc.x == kCellOut ? run2[k] : cellrun[kc.x];
+}
 
 template <bool LAYOUT>
 __device__ __forceinline__ uint32_t nine_runs(const RunBounds& rb, float px, float py, float xoff,
@@ -1926,10 +1935,9 @@ __device__ __forceinline__ uint32_t nine_runs(const RunBounds& rb, float px, flo
     } else {
 #pragma unroll
       for (int o = 0; o < 9; ++o) {
-        const uint2* q = in ? rb.cellrun + grid_enum_xy(rb.g, x + (uint32_t)kGridOff[o][0],
-                                                        y + (uint32_t)kGridOff[o][1])
-                            : rb.run2 + grid_key(cx, cy, o, N);
-        const uint2 v = *q;
+        const uint2 v = in ? rb.cellrun[grid_enum_xy(rb.g, x + (uint32_t)kGridOff[o][0],
+                                                     y + (uint32_t)kGridOff[o][1])]
+                           : key_run(rb.key_cell, rb.cellrun, rb.run2, rb.epoch, grid_key(cx, cy, o, N));
         s[o] = v.x;
         e[o] = v.y;
       }
@@ -2922,7 +2930,7 @@ __global__ __launch_bounds__(kBlock) void sph_lookup_translate_kernel(const uint
 __global__ __launch_bounds__(kBlock) void sph_count_kernel(const rps_config* __restrict__ cfg,
                                                            const uint32_t* __restrict__ offsets,
                                                            const uint32_t* __restrict__ ends,
-                                                           const uint2* __restrict__ run2,
+                                                           const RunBounds rb, bool layout,
                                                            const f2* __restrict__ pp_s,
                                                            uint32_t p_slots,
                                                            unsigned long long* __restrict__ out) {
@@ -2936,9 +2944,10 @@ __global__ __launch_bounds__(kBlock) void sph_count_kernel(const rps_config* __r
     const int32_t cy = f32_to_i32((p[1] + cfg->screen_bounds[3]) / r);
     for (int o = 0; o < 9; ++o) {
       const uint32_t key = grid_key(cx, cy, o, N);
-      const uint32_t s0 = run2 ? run2[key].x : offsets[key];  // storage runs with the layout
+      const uint2 kr = layout ? key_run(rb.key_cell, rb.cellrun, rb.run2, rb.epoch, key)  // storage runs
+                              : make_uint2(offsets[key], ends[key]);
+      const uint32_t s0 = kr.x, e0 = kr.y;
       if (s0 >= N) continue;
-      const uint32_t e0 = run2 ? run2[key].y : ends[key];
       scanned += e0 - s0;
       for (uint32_t j = s0; j < e0; ++j) {
         const f2 q = pp_s[j];
@@ -2978,11 +2987,11 @@ __global__ __launch_bounds__(kBlock) void sph_count_kernel(const rps_config* __r
 //       indices}; runs whose first particle lies outside the grid (or
 //       longer than kRunScan) go to a list (the reference's offsets are rebuilt on readback);
 //   block counts (256 cells) and one-workgroup scan: block bases; listed runs after the grid's;
-//   write (cell order): each owned run gets the next storage range -> run2[key], cellrun[cell];
+//   write (cell order): each owned run gets the next storage range -> cellrun[cell];
 //       then pass 4's prediction for the block's storage range, in storage order; cells
 //       owning no run are marked;
-//   fixup (cell order): marked cells take their key's run from run2 (a key shared by several
-//       cells belongs to one of them).
+//   fixup (cell order): marked cells take their key's run (key_run: through the key's owner
+//       recorded by the runs kernel; a key shared by several cells belongs to one of them).
 // Cells are enumerated in 8 x 8 tiles (column by column inside a tile), tiles row-major over
 // the screen's cell range.
 
@@ -3012,7 +3021,7 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* t
 }
 
 // Each run's length and owner cell (the layout's replacement for pass 3: the scans find runs
-// through cellrun / run2, and the reference's offsets are rebuilt on debug readback).  Every
+// through cellrun / key_run, and the reference's offsets are rebuilt on debug readback).  Every
 // run's last slot also records the run's end by key (run_end), so the scan kernel sizes a
 // listed run with one load whatever its length.
 __global__ __launch_bounds__(kBlock) void sph_runs_kernel(SphLayoutArgs a, const rps_config* __restrict__ cfg,
@@ -3026,10 +3035,9 @@ __global__ __launch_bounds__(kBlock) void sph_runs_kernel(SphLayoutArgs a, const
   const uint32_t prev = valid && t > 0u ? lookup[t - 1u].x : 0xFFFFFFFFu;
   const uint32_t next = t + 1u < n ? lookup[t + 1u].x : ~e.x;
   if (valid && next != e.x) a.run_end[e.x] = t + 1u;
-  if (valid) a.run2[t] = make_uint2(0xFFFFFFFFu, 0u);  // no run for key t until the scan / write kernels
   const bool start = valid && e.x != prev;
-  // The bitmap of keys with a run (the fixup gathers run2 only for those: almost no empty cell's
-  // key has one).  Keys rise along the wave, so lanes sharing a 32-key word are adjacent: an
+  // The bitmap of keys with a run (the fixup looks a key up only where its bit is set: almost no
+  // empty cell's key has a run).  Keys rise along the wave, so lanes sharing a 32-key word are adjacent: an
   // OR-scan within each word's segment, one atomicOr per word and wave.
   {
     const uint32_t word = valid ? e.x >> 5 : 0xFFFFFFFFu;
@@ -3068,7 +3076,11 @@ __global__ __launch_bounds__(kBlock) void sph_runs_kernel(SphLayoutArgs a, const
   const int32_t cx = f32_to_i32((s[0] + cfg->screen_bounds[1]) / r);
   const int32_t cy = f32_to_i32((s[1] + cfg->screen_bounds[3]) / r);
   const uint32_t c = cell_key(cx, cy, cfg->particle_count) == e.x ? grid_enum(a.g, cx, cy) : kCellOut;
-  if (c == kCellOut || len > kRunScan) {
+  // The key's owner (keys rise along the wave: these stores share few lines), tagged with the
+  // build's epoch, so no pass resets key_cell.
+  const bool listed = c == kCellOut || len > kRunScan;
+  a.key_cell[e.x] = make_uint2(listed ? kCellOut : c, a.epoch);
+  if (listed) {
     a.out_runs[atomicAdd(a.n_out, 1u)] = make_uint2(t, 0u);  // placed by the scan kernel
   } else {
     a.cell_info[2u * c] = make_uint4(t, len | a.epoch << 8, idx[0], idx[1]);
@@ -3165,11 +3177,7 @@ __global__ __launch_bounds__(kBlock) void sph_layout_write_kernel(SphLayoutArgs 
   for (uint32_t r = 0; r < len && rel + r < kSlotMap; ++r) lcell[rel + r] = (uint8_t)threadIdx.x;
   if (in) {
     if (len) {
-      int32_t cx, cy;
-      grid_cell(a.g, e, cx, cy);  // the owner's key is its cell's key (sph_runs_kernel)
-      const uint2 run = make_uint2(b0 + rel, b0 + rel + len);
-      a.run2[cell_key(cx, cy, N)] = run;
-      a.cellrun[e] = run;
+      a.cellrun[e] = make_uint2(b0 + rel, b0 + rel + len);
     } else {
       a.cellrun[e] = make_uint2(kCellPending, 0u);
     }
@@ -3213,7 +3221,8 @@ __global__ __launch_bounds__(kBlock) void sph_layout_write_kernel(SphLayoutArgs 
     lookup[k].y = kPidFlag | predict_slot(cfg, st, sl, k, lookup[k].y, idx_prev, bin_prev);
 }
 
-// Cells owning no run take their key's storage run from run2 (complete after the write pass).
+// Cells owning no run take their key's storage run (key_run; the owners' cellrun entries are
+// complete after the write pass).
 // The listed-run count goes back to 0 for the next frame's runs kernel.
 __global__ __launch_bounds__(kBlock) void sph_layout_fixup_kernel(SphLayoutArgs a, uint32_t N) {
   const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
@@ -3223,7 +3232,8 @@ __global__ __launch_bounds__(kBlock) void sph_layout_fixup_kernel(SphLayoutArgs 
     int32_t cx, cy;
     grid_cell(a.g, c, cx, cy);
     const uint32_t k = cell_key(cx, cy, N);
-    a.cellrun[c] = (a.keybits[k >> 5] >> (k & 31u)) & 1u ? a.run2[k] : make_uint2(0xFFFFFFFFu, 0u);
+    a.cellrun[c] = (a.keybits[k >> 5] >> (k & 31u)) & 1u ? key_run(a.key_cell, a.cellrun, a.run2, a.epoch, k)
+                                                         : make_uint2(0xFFFFFFFFu, 0u);
   }
 }
 
@@ -3501,8 +3511,8 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
   // Slot-resident state: the previous layout frame's sim wrote the bin entries (key, slot).
   // Without the layout, the previous active frame's sim wrote (key, i) for the current state and
   // config (SphBuffers::pkeys): the head reads them instead of keying the positions.
-  const SortBin bin{b.cfg, b.st, b.offsets, b.n, b.lay.run2,
-                    b.resident || b.pkeys ? b.bin_next : nullptr, !b.resident && b.pkeys};
+  const SortBin bin{b.cfg, b.st, b.offsets, b.n, b.resident || b.pkeys ? b.bin_next : nullptr,
+                    !b.resident && b.pkeys};
   if (csort_ok(b)) return launch_sph_csort(b, bin, stages, s, launches);
   if (stages == 0) {  // P == 1: nothing to sort, only bin
     hipLaunchKernelGGL((sph_sort_local_kernel<true, 1>), dim3(1), dim3(64), 0, s, b.lookup, 1u, 1u, 0u,
@@ -3637,7 +3647,8 @@ int sph_batch(bool density, uint32_t p, int forced, bool layout) {
 }
 
 static RunBounds run_bounds(const SphBuffers& b) {
-  return RunBounds{b.offsets, b.ends, b.lay.cellrun, b.lay.run2, b.lay.g, b.lay.keybits};
+  return RunBounds{b.offsets, b.ends, b.lay.cellrun, b.lay.run2, b.lay.key_cell, b.lay.epoch, b.lay.g,
+                   b.lay.keybits};
 }
 
 // Workgroups of the long-scan kernels (4 waves each, a wave per queued slot in turn).
@@ -3826,7 +3837,7 @@ uint32_t sph_count_blocks(uint32_t p_slots) { return blocks_for(p_slots); }
 
 hipError_t launch_sph_count(const SphBuffers& b, unsigned long long* out, hipStream_t s) {
   hipLaunchKernelGGL(sph_count_kernel, dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg,
-                     b.offsets, b.ends, b.layout ? b.lay.run2 : nullptr, b.sl.pp_s, b.p, out);
+                     b.offsets, b.ends, run_bounds(b), b.layout, b.sl.pp_s, b.p, out);
   return hipGetLastError();
 }
 
