@@ -63,6 +63,7 @@ struct rps_ctx {
   uint8_t sph_batch_d = 0, sph_batch_s = 0;  // forced scan batches (0: by size)
   SphLayoutArgs lay{};     // spatial record layout (RPS_SPH_LAYOUT, P >= 2^20 by default): arrays
   uint32_t cell_cap = 0;   // their cell capacity (0: no layout)
+  uint8_t* own_buf = nullptr;  // P != N with the layout: SphSlots::own_s of resident frames
   bool layout_last = false;  // the last active frame used the layout (slot records in storage order)
   bool last_frame_active = false;  // the most recent frame ran passes 4-5 (rps_sph_frame_cost)
   unsigned long long* d_count = nullptr;  // rps_sph_frame_cost's per-workgroup counts (SPH)
@@ -523,6 +524,8 @@ int step_sph_sim(rps_ctx* ctx, bool layout, const SphGrid& g) {
     }
   }
   ++ctx->sl.owner_epoch;  // this active frame's owner claims (SphSlots::owner)
+  // P != N: a slot-resident layout frame's owners are its unflagged entries (SphSlots::own_s)
+  ctx->sl.own_s = ctx->own_buf && layout && ctx->resident ? ctx->own_buf : nullptr;
   SphBuffers b = sph_buffers(ctx);
   if (layout)
     RPS_HIP(ctx, launch_sph_layout_pre(b, ctx->stream));
@@ -684,6 +687,7 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     slots.push_back({(void**)&ctx->ends, align_up(n * sizeof(uint32_t), 256)});
     slots.push_back({(void**)&ctx->sl.nbr_mask, align_up(2 * P * sizeof(uint64_t), 256)});
     if (P != n) slots.push_back({(void**)&ctx->sl.owner, align_up(n * sizeof(uint64_t), 256)});
+    if (P != n && lay_ok) slots.push_back({(void**)&ctx->own_buf, align_up(P, 256)});
     // Long scans one per wave (rps_kernels.hip, kLongScan): P != N, where the reference's pad
     // hazard grows long duplicate runs.  RPS_SPH_LONGQ=0 keeps them in their lanes (A/B).
     if (P != n && env_int("RPS_SPH_LONGQ", 1) != 0) {

@@ -120,6 +120,11 @@ struct SphSlots {
   // neighbour entry) skip the density too.
   uint64_t* owner;
   uint32_t owner_epoch;  // the last active frame's (1, 2, ...; the arena's zeros are epoch 0)
+  // P != N, when the last active frame was a slot-resident layout frame (else nullptr): there
+  // every stale pad entry is flagged (kPidFlag), so each particle has exactly one unflagged
+  // entry, and its slot owns the particle: own_s[t] = 1 <=> slot t's entry is unflagged (written
+  // in slot order by the write kernel; owner[] is then neither claimed nor read).
+  uint8_t* own_s;
   // P != N only (else nullptr): the slots whose nine runs hold more than kLongScan entries,
   // appended by the density pass as {slot + 1, predicted x, y bits, 0} and computed one per
   // wave by the long-scan kernels (rps_kernels.hip).  P + 1 entries, {0, ...} past the last

@@ -1818,7 +1818,7 @@ __device__ __forceinline__ void owner_claim(const SphSlots& sl, uint32_t i, uint
   atomicMax(reinterpret_cast<unsigned long long*>(sl.owner + i), (unsigned long long)owner_tag(sl, t));
 }
 __device__ __forceinline__ bool owner_is(const SphSlots& sl, uint32_t i, uint32_t t) {
-  return sl.owner[i] == owner_tag(sl, t);
+  return sl.own_s ? sl.own_s[t] != 0u : sl.owner[i] == owner_tag(sl, t);
 }
 
 // apply_gravity (wgsl:397-400) and the prediction (:402-405) of particle i into slot u.
@@ -1848,7 +1848,8 @@ __device__ __forceinline__ uint32_t predict_slot(const rps_config* __restrict__ 
   const Payload pl = resolve_payload(e, idx_prev, bin_prev);
   const f4 s = st[pl.state];
   const uint32_t i = pl.pid;
-  if (sl.owner) owner_claim(sl, i, u);  // P != N: the lowest slot of particle i owns it
+  if (sl.own_s) sl.own_s[u] = (e & kPidFlag) ? 0u : 1u;  // P != N, resident: the unflagged entry
+  else if (sl.owner) owner_claim(sl, i, u);  // P != N: the lowest slot of particle i owns it
   const float dt = cfg->fixed_delta_time;
   const float qx = s[2] + 0.0f * dt;  // apply_gravity, wgsl:397-400
   const float qy = s[3] + (-cfg->gravity) * dt;
