@@ -2480,7 +2480,10 @@ __device__ __forceinline__ void sim_finish(const rps_config* __restrict__ cfg, c
     const float r = cfg->smoothing_radius;
     const int32_t cx = f32_to_i32((ox + cfg->screen_bounds[1]) / r);
     const int32_t cy = f32_to_i32((oy + cfg->screen_bounds[3]) / r);
-    bin_next[i] = make_uint2(cell_key(cx, cy, cfg->particle_count), t);
+    // a scattered 8-B store (particle order): nontemporal, so it does not take the L2 lines the
+    // neighbour gathers use (2^22 frame 0.9035 -> 0.8936 ms, 2^21 0.4964 -> 0.4933)
+    __builtin_nontemporal_store((uint64_t)cell_key(cx, cy, cfg->particle_count) | ((uint64_t)t << 32),
+                                reinterpret_cast<uint64_t*>(bin_next + i));
   } else {
     st[i] = f4{ox, oy, qx, qy};
     if (bin_next) {  // the next frame's bin entry in particle order (SphBuffers::pkeys)
