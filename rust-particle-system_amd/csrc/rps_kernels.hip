@@ -1043,13 +1043,22 @@ __device__ __forceinline__ void quad_swap_bit(uint2 (&v)[8], uint32_t t) {
 // Store a lane's eight consecutive entries [8t, 8t + 8) of `tile` in whole 64-B segments: the
 // lane quad transposes its 16-B pairs, so store i of lane l writes pair l of lane i's eight and
 // each store instruction fills one 64-B segment per quad (lane-strided 16-B stores would send
-// four partial write requests per segment).
+// four partial write requests per segment).  NT: nontemporal stores, for the 8192-entry tiles
+// (P >= 2^21) whose lookup outgrows the L2s anyway (2^22 frame 0.8890 -> 0.8855 ms, 2^21
+// 0.4885 -> 0.4832, profiles/r05_sort_ntstore_ab.txt); smaller lookups stay cached for the
+// next launch.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <bool NT = false>
 __device__ __forceinline__ void store_eight(uint2* tile, uint32_t t, uint2 (&v)[8]) {
   quad_swap_bit<1, kDppXor2>(v, t);
   quad_swap_bit<0, kDppXor1>(v, t);
-  uint4* out = reinterpret_cast<uint4*>(tile + 32u * (t >> 2) + 2u * (t & 3u));
+  u32x4* out = reinterpret_cast<u32x4*>(tile + 32u * (t >> 2) + 2u * (t & 3u));
 #pragma unroll
-  for (int i = 0; i < 4; ++i) out[4 * i] = make_uint4(v[2 * i].x, v[2 * i].y, v[2 * i + 1].x, v[2 * i + 1].y);
+  for (int i = 0; i < 4; ++i) {
+    const u32x4 q{v[2 * i].x, v[2 * i].y, v[2 * i + 1].x, v[2 * i + 1].y};
+    if (NT) __builtin_nontemporal_store(q, out + 4 * i);
+    else out[4 * i] = q;
+  }
 }
 
 
@@ -1134,7 +1143,7 @@ __global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_e
     for (int i = 0; i < 8; ++i) v[i] = lds[a + i];
     xlane_pass<kDppXor1, false>(v, (t & 1u) == 0u);  // stride 8: entry i of the left lane vs the right's
     group_passes<3>(v);  // strides 4, 2, 1 inside the lane's eight
-    store_eight(tile, t, v);
+    store_eight<TLOG == 13>(tile, t, v);
   }
 }
 
@@ -1285,7 +1294,7 @@ __global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_e
   // The bin's LDS image was read back by this lane only ([8t, 8t + 8)); its other entries were
   // written by other waves before the barrier above, so stage 5's first write is safe.
   head_stages<5, TLOG>(lds, t, v);
-  store_eight(lookup + base0, t, v);
+  store_eight<TLOG == 13>(lookup + base0, t, v);
 }
 
 // ---------------------------------------------------------------------------------------
