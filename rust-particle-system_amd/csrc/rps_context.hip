@@ -518,7 +518,7 @@ int step_sph_sim(rps_ctx* ctx, bool layout, const SphGrid& g) {
     // cell_info and key_cell records carry the build's epoch (the arena's zeros are epoch 0); at
     // the wrap the old records are cleared so none can match a reused epoch
     if (++ctx->lay.epoch >= (1u << 24)) {
-      RPS_HIP(ctx, hipMemsetAsync(ctx->lay.cell_info, 0, (size_t)ctx->cell_cap * 2 * sizeof(uint4), ctx->stream));
+      RPS_HIP(ctx, hipMemsetAsync(ctx->lay.cell_info, 0, (size_t)ctx->cell_cap * sizeof(uint4), ctx->stream));
       RPS_HIP(ctx, hipMemsetAsync(ctx->lay.key_cell, 0, (size_t)ctx->n * sizeof(uint2), ctx->stream));
       ctx->lay.epoch = 1;
     }
@@ -714,7 +714,7 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
       // ~0.52), and at least the reference's default 1920 x 1080 viewport (~27 000 cells).
       ctx->cell_cap = (uint32_t)std::max<size_t>(n, 1u << 16);
       const size_t cap = ctx->cell_cap;
-      slots.push_back({(void**)&ctx->lay.cell_info, align_up(cap * 2 * sizeof(uint4), 256)});
+      slots.push_back({(void**)&ctx->lay.cell_info, align_up(cap * sizeof(uint4), 256)});
       slots.push_back({(void**)&ctx->lay.cellrun, align_up(cap * sizeof(uint2), 256)});
       slots.push_back({(void**)&ctx->lay.run2, align_up(n * sizeof(uint2), 256)});
       slots.push_back({(void**)&ctx->lay.part, align_up((cap / 256 + 2) * sizeof(uint32_t), 256)});

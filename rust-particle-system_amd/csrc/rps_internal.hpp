@@ -143,8 +143,8 @@ struct SphGrid {
 };
 struct SphLayoutArgs {
   SphGrid g;
-  uint4* cell_info;    // 2 x cells: {first slot, length | epoch << 8, 6 particle indices} of the
-                       //   run a cell owns (another epoch: none; so it is never reset)
+  uint4* cell_info;    // cells: {first slot, length | epoch << 8, 2 particle indices} of the run
+                       //   a cell owns (another epoch: none; so it is never reset)
   uint32_t epoch;      // this layout build's (1 ... 2^24 - 1; cell_info, key_cell cleared at the wrap)
   uint2* cellrun;      // cells: storage {start, end} of the cell's key's run (start >= N: none)
   uint2* run2;         // N: storage {start, end} of the listed runs, by key (never reset)

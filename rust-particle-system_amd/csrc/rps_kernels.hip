@@ -1750,7 +1750,7 @@ __global__ __launch_bounds__(kBlock) void sph_offsets_kernel(const uint2* __rest
 constexpr uint32_t kCellOut = 0xFFFFFFFFu;
 constexpr uint32_t kCellPending = 0xFFFFFFFEu;  // cellrun entry the fixup resolves by key
 constexpr uint32_t kRunScan = 32u;               // longest run a runs-kernel lane measures itself
-constexpr uint32_t kRunIdx = 6u;                 // particle indices a run's cell_info records
+constexpr uint32_t kRunIdx = 2u;                 // particle indices a run's cell_info records
 
 #ifndef RPS_CELL_TILE_LOG
 #define RPS_CELL_TILE_LOG 3  // 8 x 8 cells per tile (4 x 4: equal, 16 x 16: slower)
@@ -3101,8 +3101,7 @@ __global__ __launch_bounds__(kBlock) void sph_runs_kernel(SphLayoutArgs a, const
   if (listed) {
     a.out_runs[atomicAdd(a.n_out, 1u)] = make_uint2(t, 0u);  // placed by the scan kernel
   } else {
-    a.cell_info[2u * c] = make_uint4(t, len | a.epoch << 8, idx[0], idx[1]);
-    a.cell_info[2u * c + 1u] = make_uint4(idx[2], idx[3], idx[4], idx[5]);
+    a.cell_info[c] = make_uint4(t, len | a.epoch << 8, idx[0], idx[1]);
   }
 }
 
@@ -3114,7 +3113,7 @@ __device__ __forceinline__ uint32_t owned_len(const SphLayoutArgs& a, uint32_t v
 // Run lengths owned by each 256-cell block.
 __global__ __launch_bounds__(kBlock) void sph_layout_count_kernel(SphLayoutArgs a) {
   const uint32_t e = blockIdx.x * kBlock + threadIdx.x;
-  const uint32_t len = owned_len(a, e < a.g.cells ? a.cell_info[2u * e].y : 0u);
+  const uint32_t len = owned_len(a, e < a.g.cells ? a.cell_info[e].y : 0u);
   uint32_t tot;
   block_exclusive_scan<kBlock>(len, &tot);
   if (threadIdx.x == 0) a.part[blockIdx.x] = tot;
@@ -3178,8 +3177,7 @@ __global__ __launch_bounds__(kBlock) void sph_layout_write_kernel(SphLayoutArgs 
   __shared__ uint8_t lcell[kSlotMap];
   const uint32_t e = blockIdx.x * kBlock + threadIdx.x;
   const bool in = e < a.g.cells;
-  const uint4 i0 = in ? a.cell_info[2u * e] : make_uint4(0u, 0u, 0u, 0u);
-  const uint4 i1 = in ? a.cell_info[2u * e + 1u] : make_uint4(0u, 0u, 0u, 0u);
+  const uint4 i0 = in ? a.cell_info[e] : make_uint4(0u, 0u, 0u, 0u);
   const uint32_t len = owned_len(a, i0.y);
   const uint32_t b0 = a.part[blockIdx.x];
   uint32_t tot;
@@ -3188,10 +3186,6 @@ __global__ __launch_bounds__(kBlock) void sph_layout_write_kernel(SphLayoutArgs 
   lsrc[threadIdx.x] = i0.x;
   lidx[0][threadIdx.x] = i0.z;
   lidx[1][threadIdx.x] = i0.w;
-  lidx[2][threadIdx.x] = i1.x;
-  lidx[3][threadIdx.x] = i1.y;
-  lidx[4][threadIdx.x] = i1.z;
-  lidx[5][threadIdx.x] = i1.w;
   for (uint32_t r = 0; r < len && rel + r < kSlotMap; ++r) lcell[rel + r] = (uint8_t)threadIdx.x;
   if (in) {
     if (len) {
