@@ -60,9 +60,13 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=1 << 22, help="CPU-baseline particles")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=0x5EED)
-    ap.add_argument("--allpairs-n", type=int, default=1 << 22,
-                    help="global particles of the all-pairs N-body side measurement (0: skip)")
-    ap.add_argument("--allpairs-steps", type=int, default=2)
+    ap.add_argument("--allpairs-n", type=int, default=1 << 24,
+                    help="global particles of the all-pairs N-body side measurement (BASELINE.json "
+                         "configs[3], C4: 2^24; 0: skip)")
+    ap.add_argument("--allpairs-steps", type=int, default=1,
+                    help="timed all-pairs steps (one C4 step is ~45 s on one MI355X)")
+    ap.add_argument("--allpairs-warmup", type=int, default=1,
+                    help="untimed all-pairs steps first (RCCL channels, code objects, clocks)")
     ap.add_argument("--allpairs-cpu-n", type=int, default=65536,
                     help="all-pairs CPU baseline size (SURVEY 8d: 65 536, every target x every source; 0: skip)")
     ap.add_argument("--sph-n", type=int, default=1 << 22,
@@ -80,11 +84,21 @@ def parse():
                     help="render-interop export (rps_export_particles) repetitions timed on the headline state; 0: skip")
     ap.add_argument("--export-after", action="store_true",
                     help="measure the export after the headline's timed region instead of before its warmup")
-    ap.add_argument("--allpairs-timeout", type=float, default=240.0,
+    ap.add_argument("--allpairs-timeout", type=float, default=300.0,
                     help="watchdog: print the headline line and exit non-zero if a side run hangs")
     ap.add_argument("--master-port", type=int, default=0,
                     help="rendezvous port when bench.py starts its own ranks (0: a free port)")
     return ap.parse_args()
+
+
+_T_START = time.perf_counter()
+
+
+def progress(d, msg):
+    """A progress line on rank 0's stderr (the JSON line stays the only stdout line): the C4
+    all-pairs side run alone is ~1.5 min without output otherwise."""
+    if d.rank == 0:
+        print(f"bench.py [{time.perf_counter() - _T_START:6.1f} s] {msg}", file=sys.stderr, flush=True)
 
 
 WATCHDOG_RC = 3  # a side run hung: the headline line is printed, the process still fails
@@ -269,11 +283,13 @@ def allpairs(rps, args, d):
         if d.dist:  # under a launcher, even with one rank: the library's own RCCL all-gather
             ctx.comm_init(d.rank, d.world, d.broadcast_bytes(rps.comm_unique_id() if d.rank == 0 else b""))
         ctx.init_scatter(args.seed)
-        ctx.step(1)  # warm: RCCL channels, LDS kernels
+        if args.allpairs_warmup > 0:
+            ctx.step(args.allpairs_warmup)  # warm: RCCL channels, LDS kernels
         ctx.sync()
         d.sync_device()
         d.barrier()
         ctx.set_profiling(1)
+        progress(d, f"allpairs: {args.allpairs_steps} timed step(s) of {n} targets x {ng} sources")
         t0 = time.perf_counter()
         ctx.step(args.allpairs_steps)
         ctx.sync()
@@ -293,8 +309,11 @@ def allpairs(rps, args, d):
     flop = 20.0 * float(n) * ng  # per rank per step (GPU Gems 3 convention, rsqrt = 4)
     tf = flop / (kms * 1e-3) / 1e12
     peak_at_clk = FP32_PEAK_TFLOPS * clk_mhz / FP32_PEAK_CLOCK_MHZ
-    return {"workload": f"all-pairs softened gravity, {ng} global particles, index-sharded x{d.world}",
-            "scaling": "strong", "steps": args.allpairs_steps, "ms_per_step": el * 1e3 / args.allpairs_steps,
+    cfg_name = {1 << 24: "C4 (BASELINE.json configs[3])", 1 << 27: "C5 (BASELINE.json configs[4])"}.get(ng, "")
+    return {"workload": f"all-pairs softened gravity, {ng} global particles, index-sharded x{d.world}"
+                        + (f" -- {cfg_name}" if cfg_name else ""),
+            "particles": ng, "particles_per_rank": n, "interactions_per_step": float(ng) * ng,
+            "scaling": "strong", "steps": args.allpairs_steps, "warmup": args.allpairs_warmup, "ms_per_step": el * 1e3 / args.allpairs_steps,
             "interactions_per_s": inter / el, "force_kernel_ms": kms,
             "roofline": {"bound": "valu", "achieved": tf, "peak": FP32_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": tf / FP32_PEAK_TFLOPS,
@@ -595,6 +614,7 @@ def run_sides(rps, args, d, line, keys):
             print(f"bench.py: side run '{key}' hung; exiting {WATCHDOG_RC}", file=sys.stderr, flush=True)
             os._exit(WATCHDOG_RC)
 
+        progress(d, f"side run '{key}'")
         timer = threading.Timer(args.allpairs_timeout, _watchdog)
         timer.daemon = True
         timer.start()
@@ -622,6 +642,7 @@ def main():
     run_sides(rps, args, d, early, first)
 
     n, id_offset, n_global = shard(args, d)
+    progress(d, f"headline: {n} particles on this rank, {args.warmup} warm-up + {args.steps} timed steps")
     cfg, ext = workload(rps, n_global)
     wl = f"C3-{n_global:.0e}-4att-drag-respawn-euler".replace("e+0", "e").replace("e+", "e")
     ctx = rps.Context(n, rps.MODE_STREAM, device=d.local if d.dist else 0,
@@ -725,6 +746,7 @@ def main():
     if export is not None:
         line["export"] = export
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
+        progress(d, "cpu_baseline")
         line["cpu_baseline"] = cpu_baseline(rps, args, cfg, ext)
     line.update(early)
     run_sides(rps, args, d, line, [k for k in SIDES if k not in first])

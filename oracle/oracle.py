@@ -55,6 +55,7 @@ def lib(omp: bool = False) -> ctypes.CDLL:
         "orc_init_scatter": (None, [_P, _P, _U64, _U64, _U64, _U32, _P, _P, _P, _P, _P, _U64]),
         "orc_nbody_accel": (None, [_P, _P, _P, _U64, _U64, _U64, _P, _P]),
         "orc_nbody_accel_ref": (None, [_P, _P, _P, _U64, _U64, _U64, _P, _P, _P]),
+        "orc_nbody_accel_ref_idx": (None, [_P, _P, _P, _U64, _P, _U64, _P, _P, _P]),
         "orc_nbody_accel_f32_omp": (None, [_P, _P, _P, _U64, _U64, _U64, _P, _P, _I]),
         "orc_nbody_integrate": (None, [_P, _P, _P, _P, _P, _P, _P, _P, _U64]),
         "orc_sph_bin": (None, [_P, _P, _P, _P, _P, _U32]),
@@ -193,11 +194,12 @@ def stream_step_omp(cfg, ext, soa, active_step, id_offset=0, threads=0, clock=No
                                       _p(exp), len(soa["x"]), threads)
 
 
-def init_scatter(cfg, ext, seed, n, id_offset=0, global_count=None, life=True, clock=0):
+def init_scatter(cfg, ext, seed, n, id_offset=0, global_count=None, life=True, clock=0, omp=False):
+    """omp=True: the OpenMP build (particles independent: the same bits, for 10^8 particles)."""
     global_count = global_count or (id_offset + n)
     soa = {k: np.zeros(n, np.float32) for k in ("x", "y", "vx", "vy")}
     soa["exp"] = np.zeros(n, np.uint16) if life else None
-    lib().orc_init_scatter(_ref(cfg), _ref(ext), seed, id_offset, global_count, clock & 0xFFFFFFFF,
+    lib(omp=omp).orc_init_scatter(_ref(cfg), _ref(ext), seed, id_offset, global_count, clock & 0xFFFFFFFF,
                            _p(soa["x"]), _p(soa["y"]), _p(soa["vx"]), _p(soa["vy"]), _p(soa["exp"]), n)
     soa["life"] = life_from_exp(soa["exp"], clock, cfg.fixed_delta_time) if life else None
     return soa
@@ -227,6 +229,27 @@ def nbody_accel_ref(ext, sx, sy, t0=0, nt=None, threads=0):
     if threads:
         L.orc_set_threads(threads)
     L.orc_nbody_accel_ref(_ref(ext), _p(sx), _p(sy), len(sx), t0, nt, _p(ax), _p(ay), _p(ab))
+    return ax, ay, ab
+
+
+def nbody_accel_ref_idx(ext, sx, sy, idx, threads=0):
+    """nbody_accel_ref's bits for the targets `idx` (any spread): eight targets per iteration
+    vectorised over the targets, each summing its sources in index order.  Returns (ax, ay,
+    abs_sum)."""
+    sx = np.ascontiguousarray(sx, np.float32)
+    sy = np.ascontiguousarray(sy, np.float32)
+    idx = np.ascontiguousarray(idx, np.uint64)
+    if len(idx) and int(idx.max()) >= len(sx):
+        raise ValueError("target index out of range")
+    nt = len(idx)
+    ax = np.zeros(nt, np.float32)
+    ay = np.zeros(nt, np.float32)
+    ab = np.zeros(nt, np.float64)
+    L = lib(omp=True)
+    if threads:
+        L.orc_set_threads(threads)
+    if nt:
+        L.orc_nbody_accel_ref_idx(_ref(ext), _p(sx), _p(sy), len(sx), _p(idx), nt, _p(ax), _p(ay), _p(ab))
     return ax, ay, ab
 
 

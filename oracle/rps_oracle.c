@@ -449,6 +449,9 @@ void orc_init_scatter(const rps_config* cfg, const rps_ext_config* ext, uint64_t
   const float y_sd = (y_max - y_min) * 0.125f;
   const float inv_count = (float)global_count;
   uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  /* Particles are independent: the OpenMP build (orc_init_scatter through lib(omp=True), the
+   * full-size GPU tests) returns the serial checker's bits. */
+#pragma omp parallel for schedule(static)
   for (uint64_t i = 0; i < n; ++i) {
     uint64_t g = id_offset + i;
     float t = (float)g / inv_count;
@@ -523,6 +526,52 @@ void orc_nbody_accel_ref(const rps_ext_config* ext, const float* sx, const float
     ax[ii] = (float)(accx * gm);
     ay[ii] = (float)(accy * gm);
     abs_sum[ii] = acca * (double)gm;
+  }
+}
+
+/* orc_nbody_accel_ref for an explicit list of target indices (the full-size GPU tests sample
+ * thousands of targets spread over every target block of a launch).  Eight targets per
+ * iteration, each with its own accumulators summing its sources in index order with the
+ * scalar function's operations (no contraction: -ffp-contract=off), so the compiler's vector
+ * lanes over the eight targets return the scalar function's bits target by target. */
+void orc_nbody_accel_ref_idx(const rps_ext_config* ext, const float* sx, const float* sy,
+                             uint64_t ns, const uint64_t* idx, uint64_t nt, float* ax, float* ay,
+                             double* abs_sum) {
+  enum { T = 8 };
+  const double eps2 = (double)(ext->nbody_softening * ext->nbody_softening);
+  const double gm = (double)ext->nbody_strength;
+  const int64_t ng = (int64_t)((nt + T - 1) / T);
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int64_t g = 0; g < ng; ++g) {
+    double xi[T], yi[T], accx[T], accy[T], acca[T];
+    for (int k = 0; k < T; ++k) {
+      const uint64_t ii = (uint64_t)g * T + (uint64_t)k;
+      const uint64_t t = idx[ii < nt ? ii : nt - 1];
+      xi[k] = (double)sx[t];
+      yi[k] = (double)sy[t];
+      accx[k] = accy[k] = acca[k] = 0.0;
+    }
+    for (uint64_t j = 0; j < ns; ++j) {
+      const double qx = (double)sx[j], qy = (double)sy[j];
+#pragma omp simd
+      for (int k = 0; k < T; ++k) {
+        const double dx = qx - xi[k], dy = qy - yi[k];
+        const double d2 = dx * dx + dy * dy;
+        const double r2 = d2 + eps2;
+        const double inv = 1.0 / sqrt(r2);
+        const double s = inv * inv * inv;
+        accx[k] += dx * s;
+        accy[k] += dy * s;
+        acca[k] += sqrt(d2) * s;
+      }
+    }
+    for (int k = 0; k < T; ++k) {
+      const uint64_t ii = (uint64_t)g * T + (uint64_t)k;
+      if (ii >= nt) break;
+      ax[ii] = (float)(accx[k] * gm);
+      ay[ii] = (float)(accy[k] * gm);
+      abs_sum[ii] = acca[k] * gm;
+    }
   }
 }
 

@@ -80,6 +80,10 @@ void orc_nbody_accel(const rps_ext_config* ext, const float* sx, const float* sy
                      uint64_t t0, uint64_t nt, float* ax, float* ay);
 void orc_nbody_accel_ref(const rps_ext_config* ext, const float* sx, const float* sy, uint64_t ns,
                          uint64_t t0, uint64_t nt, float* ax, float* ay, double* abs_sum);
+/* orc_nbody_accel_ref's bits for the targets idx[0 .. nt) (any order, any spread). */
+void orc_nbody_accel_ref_idx(const rps_ext_config* ext, const float* sx, const float* sy,
+                             uint64_t ns, const uint64_t* idx, uint64_t nt, float* ax, float* ay,
+                             double* abs_sum);
 /* The same force in f32 on every host core (bench.py's all-pairs cpu_baseline only, not a
  * checker): per target an f32 sum, vectorised by `omp simd` (its own summation order). */
 void orc_nbody_accel_f32_omp(const rps_ext_config* ext, const float* sx, const float* sy,

@@ -44,6 +44,22 @@ def test_gpus2_starts_two_ranks():
     assert line["allpairs"]["collective"].startswith("ncclAllGather")
 
 
+@pytest.mark.parametrize("gpus", [1, 8])
+def test_allpairs_default_is_c4(gpus):
+    """Without --allpairs-n the all-pairs side line is BASELINE.json configs[3] (C4): 2^24
+    particles, one timed step after one warm step, targets strong-sharded 2^24 / N per rank
+    with the library's all-gather under a launcher (8 gloo ranks here, as the driver's 8-GPU
+    node runs it)."""
+    p, lines = _run(WEAK + ["--gpus", str(gpus)], timeout=400)
+    assert p.returncode == 0, p.stderr[-3000:]
+    ap = lines[0]["allpairs"]
+    assert ap["particles"] == 1 << 24 and ap["particles_per_rank"] == (1 << 24) // gpus
+    assert "16777216 global particles" in ap["workload"] and "C4" in ap["workload"]
+    assert ap["steps"] == 1 and ap["warmup"] == 1 and ap["scaling"] == "strong"
+    assert ap["collective"].startswith("ncclAllGather") == (gpus > 1)
+    assert ap["roofline"]["peak"] == 157.3 and ap["roofline"]["unit"] == "TFLOP/s"
+
+
 def test_single_process_defaults_to_one_gpu():
     p, lines = _run(WEAK + ["--allpairs-n", "0"])
     assert p.returncode == 0, p.stderr[-3000:]

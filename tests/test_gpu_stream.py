@@ -250,6 +250,68 @@ def test_full_size_sampled_parity(gpu, orc):
         assert_soa_bitwise(a, b, keys=KEYS_STEPS, what=f"chunk@{s} ")
 
 
+def _assert_full_state(rps, orc, ctx, ref, clock, what, chunk=1 << 24):
+    """Every particle of a 10^8 context against the oracle's arrays, bitwise, by chunks of
+    2^24 (bounded host memory): x, y, vx, vy, the exact lifetime steps left and the raw u16
+    expiries."""
+    n = len(ref["x"])
+    for s in range(0, n, chunk):
+        m = min(chunk, n - s)
+        got = _download_chunk(rps, ctx, s, m)
+        want = {k: ref[k][s:s + m] for k in ("x", "y", "vx", "vy")}
+        want["steps"] = orc.steps_from_exp(ref["exp"][s:s + m], clock)
+        assert_soa_bitwise(got, want, keys=KEYS_STEPS, what=f"{what} chunk@{s} ")
+    assert_bitwise(ctx.read_debug(rps.DEBUG_EXPIRY), ref["exp"], f"{what} expiry")
+
+
+def test_full_size_every_particle(gpu, orc):
+    """BASELINE C3 exactly as bench.py runs it (10^8 particles, 4 moving attractors, drag,
+    lifetime U(1, 5) s with Philox respawn on the emitter disc, stats every 100 steps, every
+    step active), EVERY particle checked, not a sample: the device scatter against the
+    oracle's (orc_init_scatter on the OpenMP build: the serial checker's bits), then 130 steps;
+    the two stats steps (0 and 100) run through the serial checker and their stats are compared
+    (bbox and counts exact, KE to 1e-9), the other 128 on the oracle's OpenMP build
+    (orc_stream_step_omp: the serial checker's operations per particle).  dt = 0.01 s, so the
+    1-s lifetimes expire from step 100 on and respawns are part of the compared state.  Every
+    field, the exact lifetime steps left and the raw u16 expiries, bitwise, by 2^24-particle
+    chunks."""
+    rps = gpu
+    n, steps, stats_step = 100_000_000, 130, 100
+    cfg = rps.default_particle_config(n, gravity=0.0)  # bench.py workload()
+    ext = rps.headline_ext(stats=True)
+    ext.shader_delay = 0
+    assert ext.stats_interval == stats_step
+
+    def check_stats(st, ost, k):
+        assert st.step == k and st.particles == n
+        assert st.respawned == ost.respawned
+        assert list(st.bbox) == list(ost.bbox)
+        assert abs(st.kinetic_energy - ost.kinetic_energy) <= 1e-9 * abs(ost.kinetic_energy)
+
+    with rps.Context(n, rps.MODE_STREAM, global_count=n) as ctx:
+        ctx.set_config(cfg, ext)
+        ctx.init_scatter(0x5EED)
+        ref = orc.init_scatter(cfg, ext, 0x5EED, n, global_count=n, omp=True)
+        ref["life"] = None  # the u16 expiries are the state; steps are compared exactly
+        _assert_full_state(rps, orc, ctx, ref, 0, "init")
+        due = int(np.count_nonzero(orc.steps_from_exp(ref["exp"], 0) <= steps))
+        assert due > n // 100  # respawns are part of the compared state
+        ctx.step(1)
+        check_stats(ctx.stats(), orc.stream_step(cfg, ext, ref, 0, stats=True), 0)
+        ctx.step(steps - 1)
+        ost = None
+        for k in range(1, steps):
+            if k == stats_step:
+                ost = orc.stream_step(cfg, ext, ref, k, stats=True)
+                ref["life"] = None
+            else:
+                orc.stream_step_omp(cfg, ext, ref, k)
+        assert ost.respawned > 0
+        check_stats(ctx.stats(), ost, stats_step)
+        assert ctx.counters() == (steps, steps)
+        _assert_full_state(rps, orc, ctx, ref, steps, f"step{steps}")
+
+
 def test_aos_roundtrip_and_errors(gpu):
     rps = gpu
     n = 5000
