@@ -498,6 +498,11 @@ int sph_canonical(rps_ctx* ctx) {
 // a resident frame writes its slot -> particle map to the other buffer (the sort payloads
 // refer to the current one).
 int sph_frame_begin(rps_ctx* ctx, bool layout) {
+  // Every path out of the slot-resident state runs sph_canonical, which also turns the lookup's
+  // payloads back into particle indices: the compact sort's 16-bit payloads (csort_ok) rely on
+  // it for P != N, so a broken invariant fails here instead of sorting truncated payloads.
+  if (!ctx->resident && ctx->lookup_perm)
+    return fail(ctx, RPS_ERR_DEVICE, "internal: lookup payloads left slot-resident outside a resident frame");
   if (ctx->resident && !layout) {
     const int rc = sph_canonical(ctx);
     if (rc) return rc;
@@ -1051,6 +1056,10 @@ int rps_init_scatter(rps_ctx* ctx, uint64_t seed) {
   int rc = check_ctx(ctx);
   if (rc) return rc;
   if (!ctx->have_config) return fail(ctx, RPS_ERR_INVALID_ARGUMENT, "rps_set_config first");
+  // Leaving the slot-resident state like every other particle-order write: the lookup's payloads
+  // back to particle indices (P != N: the pads unflagged) and lookup_perm cleared, so a later
+  // DEBUG_SPATIAL_LOOKUP read and the compact sort's 16-bit payloads see particle indices.
+  if ((rc = sph_canonical(ctx))) return rc;
   InitArgs a;
   a.f = fields(ctx);
   a.layout = ctx->layout;
@@ -1068,8 +1077,7 @@ int rps_init_scatter(rps_ctx* ctx, uint64_t seed) {
   a.dt = ctx->cfg.fixed_delta_time;
   a.key0 = (uint32_t)seed;
   a.key1 = (uint32_t)(seed >> 32);
-  ctx->resident = false;  // every particle rewritten in particle order
-  ctx->keys_valid = false;
+  ctx->keys_valid = false;  // every particle rewritten in particle order
   ctx->pkeys_valid = false;
   RPS_HIP(ctx, launch_init_scatter(a, ctx->stream));
   if (ctx->next)

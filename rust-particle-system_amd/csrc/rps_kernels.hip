@@ -1817,9 +1817,14 @@ __constant__ int32_t kGridOff[9][2] = {{-1, -1}, {-1, 0}, {-1, 1}, {0, -1}, {0, 
 // densities buffers are not written on the hot path; launch_sph_debug_views rebuilds them
 // from the slot records on readback.  Pad slots repeat some particle and
 // write identical values.
-// Slot ownership (P != N, SphSlots::owner): {epoch, ~slot} in one u64 per particle, claimed by
-// atomicMax, so the lowest slot of the current active frame wins and an entry of an older
-// frame loses to any claim without a reset pass (a memset launch per frame, 4.7 us at 50 000).
+// Slot ownership (P != N), two rules:
+// - Particle-order frames (no layout, or a layout frame on state in particle order) use
+//   SphSlots::owner: {epoch, ~slot} in one u64 per particle, claimed by atomicMax, so the lowest
+//   slot of the current active frame wins and an entry of an older frame loses to any claim
+//   without a reset pass (a memset launch per frame, 4.7 us at 50 000).
+// - Slot-resident layout frames (SphSlots::own_s non-null) own a particle at its unflagged
+//   entry: the pad entries carry kPidFlag | index, and own_s[t] marks slot t as the owner;
+//   owner[] is neither claimed nor read in those frames.
 __device__ __forceinline__ uint64_t owner_tag(const SphSlots& sl, uint32_t t) {
   return ((uint64_t)sl.owner_epoch << 32) | (uint64_t)(0xFFFFFFFFu - t);
 }
@@ -3507,7 +3512,11 @@ static hipError_t launch_sph_csort(const SphBuffers& b, const SortBin& bin, uint
 
 // Whether this frame's sort runs compact: 2^11 <= P <= 2^16 and every lookup payload below 2^16.
 // Only a resident frame with P != N holds flagged payloads (the pad entries the previous layout
-// frame wrote); sph_canonical unflags them before any frame that leaves the layout.
+// frame wrote).  Every path that leaves the resident state (a non-layout frame, and
+// every particle-order API call: particle and field uploads and downloads, export,
+// init_scatter) runs sph_canonical, which unflags them, and sph_frame_begin fails a frame that finds
+// slot-resident payloads outside a resident frame (tests/test_gpu_sph.py
+// test_sph_init_scatter_leaves_resident_state, test_sph_resident_state_api).
 static bool csort_ok(const SphBuffers& b) {
   return b.csort && b.p >= 2048u && b.p <= 65536u && !(b.resident && b.p != b.n);
 }

@@ -153,14 +153,15 @@ def test_sph_resident_state_frames(gpu, orc, monkeypatch, n):
                       download_at={3, 6})
 
 
-def test_sph_layout_epoch_wrap(gpu, orc, monkeypatch):
+@pytest.mark.parametrize("n", [16384, 16000])
+def test_sph_layout_epoch_wrap(gpu, orc, monkeypatch, n):
     """The layout's cell records carry the build's epoch instead of being reset each frame;
     started two builds before the 2^24 wrap, the frames across it (records cleared, epoch 1
-    again) stay bitwise."""
+    again) stay bitwise.  At 16 000 (P != N) the resident frames' own_s ownership and the pad
+    entries' flagged payloads cross the wrap too."""
     rps = gpu
     monkeypatch.setenv("RPS_SPH_LAYOUT", "2")
     monkeypatch.setenv("RPS_SPH_LAYOUT_EPOCH", str((1 << 24) - 3))
-    n = 16384
     cfg = rps.default_particle_config(n, gravity=100.0)
     _frames_vs_oracle(rps, orc, n, _blob(n, 47, spread=300.0), cfg, 5, download_at={4})
 
@@ -219,6 +220,47 @@ def test_sph_resident_state_api(gpu, orc, monkeypatch, n):
         frames(4, gated=2)
         assert_bitwise(ctx.read_debug(rps.DEBUG_SPATIAL_LOOKUP), st.lookup, "lookup after gated")
         assert_soa_bitwise(ctx.download_soa(), ref, what="after gated ")
+
+
+@pytest.mark.parametrize("n", [16384, 16000, 5000])
+def test_sph_init_scatter_leaves_resident_state(gpu, orc, monkeypatch, n):
+    """rps_init_scatter on slot-resident state: resident layout frames, then the
+    device scatter, then a gated frame (config change, SHADER_DELAY 3), a lookup readback and
+    active frames.  The scatter leaves the resident state like every particle-order write: the
+    lookup's pad payloads are particle indices again (P != N at 16 000 and 5 000, where the
+    next frames may run the compact sort on 16-bit payloads), so the gated frame's lookup is
+    the reference's, and every later frame stays bitwise."""
+    rps = gpu
+    monkeypatch.setenv("RPS_SPH_LAYOUT", "2")
+    cfg = rps.default_particle_config(n, gravity=100.0)
+    soa = _blob(n, 53, spread=300.0)
+    st = orc.SphState(n)
+    ref = copy_soa(soa)
+
+    def frames(k, gated=0):
+        for f in range(k):
+            st.grid(cfg, ref)
+            if f >= gated:
+                st.pre(cfg, ref)
+                st.sim(cfg, ref)
+
+    with rps.Context(n, rps.MODE_SPH) as ctx:
+        ctx.set_config(cfg, rps.make_ext(shader_delay=0))
+        ctx.upload_soa(soa)
+        ctx.step(3)
+        frames(3)
+        ctx.init_scatter(0x5EED)
+        init = orc.init_scatter(cfg, rps.make_ext(), 0x5EED, n, life=False)
+        ref = {k: init[k] for k in ("x", "y", "vx", "vy")}
+        cfg = rps.default_particle_config(n, gravity=80.0)
+        ctx.set_config(cfg, rps.make_ext(shader_delay=3))  # frame_count 0: frames 1, 2 gated
+        ctx.step(1)
+        frames(1, gated=1)
+        assert_bitwise(ctx.read_debug(rps.DEBUG_SPATIAL_LOOKUP), st.lookup, "lookup after init_scatter + gated")
+        ctx.step(3)
+        frames(3, gated=1)
+        assert_bitwise(ctx.read_debug(rps.DEBUG_SPATIAL_LOOKUP), st.lookup, "lookup after active frames")
+        assert_soa_bitwise(ctx.download_soa(), ref, what="after init_scatter ")
 
 
 @pytest.mark.parametrize("n", [4096, 50000])
@@ -665,10 +707,13 @@ def test_sph_particle_order_bin_entries(gpu, orc, n):
         assert_soa_bitwise(ctx.download_soa(), ref, what="after config change ")
 
 
+@pytest.mark.perf
 def test_sph_layout_clustered_runs_timing(gpu, monkeypatch):
     """Performance regression bound on the listed-run path: on the clumped 2^21 state a frame
     with the spatial layout costs at most 3x a lookup-order frame (measured ~1x,
-    tools/ab_sph.py; round 2's per-lane walk of listed runs was many times slower)."""
+    tools/ab_sph.py; round 2's per-lane walk of listed runs was many times slower).  A
+    wall-clock bound, so outside the correctness suite (RPS_PERF_TESTS=1 runs it); the
+    clumped state's correctness is test_sph_layout_clustered_runs's."""
     rps = gpu
     n = 1 << 21
     cfg, soa = _clumped_state(rps, n)
