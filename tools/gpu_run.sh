@@ -54,11 +54,14 @@ for step in "$@"; do
     prof_sph64k)
       run prof_sph64k 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_sph64k -o run --output-format csv -- python3 tools/sph_frames.py 65536 60 || exit $? ;;
     sizes)
-      # SPH frame by size (all-active frames, tools/ab_sph.py), one line per size
+      # SPH frame by size (all-active frames, tools/ab_sph.py, bench.py's window: 20 warm, 200
+      # timed), one line per size
       for n in 20000 50000 65536 100000 262144 300000 1000000 1048576 2097152 4194304; do
-        run sizes_$n 120 python tools/ab_sph.py --n $n --frames 50 --rounds 2 rust-particle-system_amd/lib/librps.so || exit $?
+        run sizes_$n 120 python tools/ab_sph.py --n $n --warm 20 --frames 200 --rounds 2 rust-particle-system_amd/lib/librps.so || exit $?
         grep "^n=" gpurun_out/sizes_$n.log >> gpurun_out/sizes.txt
       done ;;
+    curve)
+      run sph_frame_curve 300 python tools/sph_frame_curve.py || exit $? ;;
     probe)
       run hbm_probe 300 tools/hbm_probe || exit $? ;;
     *)

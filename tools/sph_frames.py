@@ -16,7 +16,7 @@ if os.environ.get("AB_LIB"):  # a variant build (tools/build_variant.sh) for A/B
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 50000
 frames = int(sys.argv[2]) if len(sys.argv) > 2 else 50
 warm = int(sys.argv[3]) if len(sys.argv) > 3 else 10
-scale = max(1.0, (n / 50000) ** 0.5)
+scale = max(1.0, (n / 50000) ** 0.5) if n > 65536 else 1.0  # bench.py: reference viewport up to 65 536
 cfg = rps.default_particle_config(n, screen_bounds=rps.screen_bounds_for(1920.0 * scale, 1080.0 * scale))
 parts = rps.setup_particles_scatter(cfg, n, seed=1)
 with rps.Context(n, rps.MODE_SPH) as ctx:
