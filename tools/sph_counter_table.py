@@ -46,8 +46,9 @@ def main():
     for r in csv.DictReader(open(find(f"cnt_trace_{n}", "kernel_stats.csv"))):
         times[short(r["Name"])] = float(r["AverageNs"]) / 1e3
     m1, m2 = counters(f"cnt_m1_{n}"), counters(f"cnt_m2_{n}")
-    log = open(os.path.join(OUT, f"cnt_trace_{n}.log")).read().strip().splitlines()
-    print(f"# SPH frame kernels at N = {n} (tools/pmc_sph_counters.sh; {log[-1] if log else ''})")
+    log = [ln for ln in open(os.path.join(OUT, f"cnt_trace_{n}.log")) if "ms/frame" in ln]
+    print(f"# SPH frame kernels at N = {n} (tools/pmc_sph_counters.sh; trace run: {log[-1].strip() if log else '?'})")
+    print("# times: that kernel trace; counters: two --pmc passes of 8 frames each, averaged per dispatch")
     print(f"{'kernel':44} {'us':>7} {'lines/ld':>8} {'L1hit':>6} {'L2hit':>6} {'TAbusy':>6} {'VALUbusy':>8} "
           f"{'wait':>5} {'instw':>5} {'valu':>5}")
     for k, us in sorted(times.items(), key=lambda kv: -kv[1]):
