@@ -28,8 +28,11 @@ def build():
     subprocess.run(["make", "-s", "-C", _HERE], check=True)
 
 
-def lib(omp: bool = False) -> ctypes.CDLL:
-    name = "librps_oracle_omp.so" if omp else "librps_oracle.so"
+def lib(omp: bool = False, fma: bool = False) -> ctypes.CDLL:
+    """The serial checker; omp: the OpenMP build (same bits); fma: the serial build with a*b+c
+    contracted into FMAs (NOT the checker: what a WGSL compiler may emit, for the schedule
+    envelope of tools/wgsl_schedule_envelope.py)."""
+    name = "librps_oracle_fma.so" if fma else "librps_oracle_omp.so" if omp else "librps_oracle.so"
     if name in _libs:
         return _libs[name]
     path = os.path.join(_BUILD, name)
@@ -63,6 +66,9 @@ def lib(omp: bool = False) -> ctypes.CDLL:
         "orc_sph_offsets": (None, [_P, _P, _U32]),
         "orc_sph_pre": (None, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _U32]),
         "orc_sph_sim": (None, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _U32]),
+        "orc_sph_pre_sched": (None, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _U32]),
+        "orc_sph_sim_sched": (None, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _U32, _P, _U32]),
+        "orc_sph_pre_stale": (None, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32]),
     }
     for k, (res, args) in sig.items():
         f = getattr(L, k)
@@ -115,13 +121,13 @@ def set_color_array(vx, vy, max_energy):
     nrm = np.where(nrm < 0, np.float32(0), nrm)
     nrm = np.where(nrm > 1, np.float32(1), nrm).astype(np.float32)
     lo = nrm < np.float32(0.5)
-    t_lo = nrm * np.float32(2.0)
-    t_hi = (nrm - np.float32(0.5)) * np.float32(2.0)
-    out = np.zeros((len(vx), 4), np.float32)
-    out[:, 0] = np.where(lo, np.float32(0), t_hi)
-    out[:, 1] = np.where(lo, t_lo, np.float32(1) - t_hi)
-    out[:, 2] = np.where(lo, np.float32(1) - t_lo, np.float32(0))
-    out[:, 3] = 1.0
+    t = np.where(lo, nrm * np.float32(2.0), (nrm - np.float32(0.5)) * np.float32(2.0)).astype(np.float32)
+    u = (np.float32(1) - t).astype(np.float32)
+    a = np.where(lo[:, None], np.float32([0, 0, 1]), np.float32([0, 1, 0])).astype(np.float32)  # blue / green
+    b = np.where(lo[:, None], np.float32([0, 1, 0]), np.float32([1, 0, 0])).astype(np.float32)  # green / red
+    out = np.ones((len(vx), 4), np.float32)
+    with np.errstate(invalid="ignore"):  # mix(a, b, t) = a * (1 - t) + b * t: NaN t -> NaN
+        out[:, :3] = a * u[:, None] + b * t[:, None]
     return out
 
 
@@ -294,13 +300,42 @@ class SphState:
         L.orc_sph_offsets(_p(self.lookup), _p(self.offsets), self.n)
         return passes
 
-    def pre(self, cfg, soa):
-        lib(omp=self.omp).orc_sph_pre(_ref(cfg), _p(soa["vx"]), _p(soa["vy"]), _p(soa["x"]), _p(soa["y"]),
+    def pre(self, cfg, soa, fma=False):
+        lib(omp=self.omp and not fma, fma=fma).orc_sph_pre(_ref(cfg), _p(soa["vx"]), _p(soa["vy"]), _p(soa["x"]), _p(soa["y"]),
                                       _p(self.lookup), _p(self.offsets), _p(self.dens), _p(self.pred), self.n)
 
-    def sim(self, cfg, soa):
-        lib(omp=self.omp).orc_sph_sim(_ref(cfg), _p(soa["x"]), _p(soa["y"]), _p(soa["vx"]), _p(soa["vy"]),
+    def sim(self, cfg, soa, fma=False):
+        lib(omp=self.omp and not fma, fma=fma).orc_sph_sim(_ref(cfg), _p(soa["x"]), _p(soa["y"]), _p(soa["vx"]), _p(soa["vy"]),
                                       _p(self.lookup), _p(self.offsets), _p(self.dens), _p(self.pred), self.n)
+
+    def copy(self):
+        """An independent copy (to run one frame under several schedules from the same state)."""
+        c = SphState.__new__(SphState)
+        c.__dict__.update({k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in self.__dict__.items()})
+        return c
+
+    # Passes 4-5 under another legal WGSL schedule (orc_sph_pre_sched / orc_sph_sim_sched): groups
+    # of `group` invocations in lockstep, one group after another in `order`; fma: the FMA-
+    # contracted build.  Test infrastructure for tools/wgsl_schedule_envelope.py, not the checker.
+    def pre_sched(self, cfg, soa, order, group, fma=False):
+        order = np.ascontiguousarray(order, np.uint32)
+        assert len(order) == (self.n + group - 1) // group
+        lib(fma=fma).orc_sph_pre_sched(_ref(cfg), _p(soa["vx"]), _p(soa["vy"]), _p(soa["x"]), _p(soa["y"]),
+                                       _p(self.lookup), _p(self.offsets), _p(self.dens), _p(self.pred), self.n,
+                                       _p(order), group)
+
+    def pre_stale(self, cfg, soa, fma=False):
+        prev = self.pred.copy()  # the previous frame's predictions, as the buffer still holds them
+        lib(fma=fma).orc_sph_pre_stale(_ref(cfg), _p(soa["vx"]), _p(soa["vy"]), _p(soa["x"]), _p(soa["y"]),
+                                       _p(self.lookup), _p(self.offsets), _p(self.dens), _p(self.pred), _p(prev),
+                                       self.n)
+
+    def sim_sched(self, cfg, soa, order, group, fma=False):
+        order = np.ascontiguousarray(order, np.uint32)
+        assert len(order) == (self.n + group - 1) // group
+        lib(fma=fma).orc_sph_sim_sched(_ref(cfg), _p(soa["x"]), _p(soa["y"]), _p(soa["vx"]), _p(soa["vy"]),
+                                       _p(self.lookup), _p(self.offsets), _p(self.dens), _p(self.pred), self.n,
+                                       _p(order), group)
 
 
 def run_steps(mode, cfg, ext, soa, nsteps, frame_count=0, active_steps=0, id_offset=0, sph=None):

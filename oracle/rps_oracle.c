@@ -125,17 +125,14 @@ void orc_set_color(float vx, float vy, float max_energy, float rgba[4]) {
   float nrm = energy / max_energy;
   nrm = nrm < 0.0f ? 0.0f : nrm; /* clamp(x, 0, 1) = min(max(x, 0), 1) */
   nrm = nrm > 1.0f ? 1.0f : nrm;
-  if (nrm < 0.5f) {
-    float t = nrm * 2.0f;
-    rgba[0] = 0.0f;
-    rgba[1] = t;
-    rgba[2] = 1.0f - t;
-  } else {
-    float t = (nrm - 0.5f) * 2.0f;
-    rgba[0] = t;
-    rgba[1] = 1.0f - t;
-    rgba[2] = 0.0f;
-  }
+  /* mix(a, b, t) = a * (1 - t) + b * t per component (WGSL's definition, computed: a NaN t
+   * makes every component NaN, 0 * NaN included). */
+  static const float A[2][3] = {{0.0f, 0.0f, 1.0f}, {0.0f, 1.0f, 0.0f}}; /* blue, green */
+  static const float B[2][3] = {{0.0f, 1.0f, 0.0f}, {1.0f, 0.0f, 0.0f}}; /* green, red */
+  const int hi = !(nrm < 0.5f);
+  const float t = hi ? (nrm - 0.5f) * 2.0f : nrm * 2.0f;
+  const float u = 1.0f - t;
+  for (int c = 0; c < 3; ++c) rgba[c] = A[hi][c] * u + B[hi][c] * t;
   rgba[3] = 1.0f;
 }
 
@@ -699,51 +696,168 @@ static inline int32_t wrap_add(int32_t a, int32_t b) {
   return (int32_t)((uint32_t)a + (uint32_t)b);
 }
 
+/* calculate_density (wgsl:207-254) of particle i at its predicted position pred[i], its
+ * neighbours' predicted positions read from `nb` (pred itself: the snapshot semantics). */
+static void density_one(const rps_config* cfg, const uint32_t* lookup, const uint32_t* offsets,
+                        const float* pred, const float* nb, uint32_t i, float* d_out,
+                        float* nd_out) {
+  const float x_max = cfg->screen_bounds[1], y_max = cfg->screen_bounds[3];
+  const float r = cfg->smoothing_radius, r2 = r * r;
+  const uint32_t N = cfg->particle_count;
+  const float px = pred[2 * i], py = pred[2 * i + 1];
+  const int32_t cx = orc_f32_to_i32((px + x_max) / r);
+  const int32_t cy = orc_f32_to_i32((py + y_max) / r);
+  float d = 0.0f, nd = 0.0f;
+  for (int o = 0; o < 9; ++o) {
+    const uint32_t key = orc_cell_key(wrap_add(cx, GRID_OFF[o][0]), wrap_add(cy, GRID_OFF[o][1]), N);
+    for (uint32_t j = offsets[key]; j < N; ++j) {
+      if (lookup[2 * j] != key) break;
+      const uint32_t oi = lookup[2 * j + 1];
+      const float qx = oi == i ? px : nb[2 * oi], qy = oi == i ? py : nb[2 * oi + 1];
+      const float dx = px - qx, dy = py - qy;
+      const float sq = dx * dx + dy * dy;
+      if (sq > r2) continue;
+      const float dist = sqrtf(sq);
+      float k1 = 0.0f, k2 = 0.0f;
+      if (!(dist >= r)) {
+        const float v = r - dist;
+        k1 = (cfg->density_kernel_norm * v) * v;            /* :145-152 */
+        k2 = ((cfg->near_density_kernel_norm * v) * v) * v; /* :163-170 */
+      }
+      d = d + k1;
+      nd = nd + k2;
+    }
+  }
+  *d_out = d;
+  *nd_out = nd;
+}
+
+/* apply_gravity (wgsl:397-400) and update_predicted_positions (:402-405) of particle i. */
+static inline void predict_one(const rps_config* cfg, float* vx, float* vy, const float* x,
+                               const float* y, float* pred, uint32_t i) {
+  const float dt = cfg->fixed_delta_time;
+  vx[i] = vx[i] + 0.0f * dt;
+  vy[i] = vy[i] + (-cfg->gravity) * dt;
+  pred[2 * i] = x[i] + vx[i] * dt;
+  pred[2 * i + 1] = y[i] + vy[i] * dt;
+}
+
 /* pre_simulation_step (wgsl:420-433): apply_gravity, update_predicted_positions for ALL
  * particles, then calculate_density (:207-254) against that snapshot. */
 void orc_sph_pre(const rps_config* cfg, float* vx, float* vy, const float* x, const float* y,
                  const uint32_t* lookup, const uint32_t* offsets, float* dens, float* pred,
                  uint32_t n) {
-  const float dt = cfg->fixed_delta_time;
-  const float gx_dt = 0.0f * dt, gy_dt = (-cfg->gravity) * dt;
 #pragma omp parallel for schedule(static)
-  for (uint32_t i = 0; i < n; ++i) {
-    vx[i] = vx[i] + gx_dt;
-    vy[i] = vy[i] + gy_dt;
-    pred[2 * i] = x[i] + vx[i] * dt;
-    pred[2 * i + 1] = y[i] + vy[i] * dt;
-  }
+  for (uint32_t i = 0; i < n; ++i) predict_one(cfg, vx, vy, x, y, pred, i);
+#pragma omp parallel for schedule(dynamic, 1024)
+  for (uint32_t i = 0; i < n; ++i) density_one(cfg, lookup, offsets, pred, pred, i, &dens[2 * i], &dens[2 * i + 1]);
+}
+
+/* calculate_pressure_force (wgsl:256-334) of particle i. */
+static void pressure_one(const rps_config* cfg, const uint32_t* lookup, const uint32_t* offsets,
+                         const float* dens, const float* pred, uint32_t i, float* fx_out,
+                         float* fy_out) {
   const float x_max = cfg->screen_bounds[1], y_max = cfg->screen_bounds[3];
   const float r = cfg->smoothing_radius, r2 = r * r;
   const uint32_t N = cfg->particle_count;
-#pragma omp parallel for schedule(dynamic, 1024)
-  for (uint32_t i = 0; i < n; ++i) {
-    const float px = pred[2 * i], py = pred[2 * i + 1];
-    const int32_t cx = orc_f32_to_i32((px + x_max) / r);
-    const int32_t cy = orc_f32_to_i32((py + y_max) / r);
-    float d = 0.0f, nd = 0.0f;
-    for (int o = 0; o < 9; ++o) {
-      const uint32_t key = orc_cell_key(wrap_add(cx, GRID_OFF[o][0]), wrap_add(cy, GRID_OFF[o][1]), N);
-      for (uint32_t j = offsets[key]; j < N; ++j) {
-        if (lookup[2 * j] != key) break;
-        const uint32_t oi = lookup[2 * j + 1];
-        const float dx = px - pred[2 * oi], dy = py - pred[2 * oi + 1];
-        const float sq = dx * dx + dy * dy;
-        if (sq > r2) continue;
-        const float dist = sqrtf(sq);
-        float k1 = 0.0f, k2 = 0.0f;
-        if (!(dist >= r)) {
-          const float v = r - dist;
-          k1 = (cfg->density_kernel_norm * v) * v;            /* :145-152 */
-          k2 = ((cfg->near_density_kernel_norm * v) * v) * v; /* :163-170 */
-        }
-        d = d + k1;
-        nd = nd + k2;
+  const float td = cfg->target_density, pm = cfg->pressure_multiplier;
+  const float nm = cfg->near_density_multiplier;
+  const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
+  const float px = pred[2 * i], py = pred[2 * i + 1];
+  const int32_t cx = orc_f32_to_i32((px + x_max) / r);
+  const int32_t cy = orc_f32_to_i32((py + y_max) / r);
+  const float rho = dens[2 * i], rhon = dens[2 * i + 1];
+  const float P = (rho - td) * pm;
+  const float Pn = rhon * nm;
+  float fx = 0.0f, fy = 0.0f;
+  for (int o = 0; o < 9; ++o) {
+    const uint32_t key = orc_cell_key(wrap_add(cx, GRID_OFF[o][0]), wrap_add(cy, GRID_OFF[o][1]), N);
+    for (uint32_t j = offsets[key]; j < N; ++j) {
+      if (lookup[2 * j] != key) break;
+      const uint32_t oi = lookup[2 * j + 1];
+      if (oi == i) continue;
+      const float dx = pred[2 * oi] - px, dy = pred[2 * oi + 1] - py;
+      const float sq = dx * dx + dy * dy;
+      if (sq > r2) continue;
+      const float dist = sqrtf(sq);
+      float dirx, diry;
+      if (dist > 0.0001f) {
+        dirx = dx / dist;
+        diry = dy / dist;
+      } else {
+        dirx = 0.0f;
+        diry = 1.0f;
       }
+      const float rj = dens[2 * oi], rnj = dens[2 * oi + 1];
+      const float Pj = (rj - td) * pm;
+      const float Pnj = rnj * nm;
+      const float pt = (P / (rho * rho)) + (Pj / (rj * rj));
+      const float npt = (Pn / (rho * rho)) + (Pnj / (rj * rnj));
+      float dk = 0.0f, ndk = 0.0f;
+      if (!(dist >= r)) {
+        const float v = r - dist;
+        dk = (-2.0f * dn) * v;         /* :154-161 */
+        ndk = ((-3.0f * ndn) * v) * v; /* :172-179 */
+      }
+      fx = fx + (dirx * pt) * dk;
+      fy = fy + (diry * pt) * dk;
+      fx = fx + (dirx * npt) * ndk;
+      fy = fy + (diry * npt) * ndk;
     }
-    dens[2 * i] = d;
-    dens[2 * i + 1] = nd;
   }
+  *fx_out = fx;
+  *fy_out = fy;
+}
+
+/* calculate_viscocity (wgsl:336-384) of particle i, own velocity (qx, qy), the neighbours'
+ * velocities read from (nvx, nvy). */
+static void viscosity_one(const rps_config* cfg, const uint32_t* lookup, const uint32_t* offsets,
+                          const float* pred, const float* nvx, const float* nvy, uint32_t i,
+                          float qx, float qy, float* wx_out, float* wy_out) {
+  const float x_max = cfg->screen_bounds[1], y_max = cfg->screen_bounds[3];
+  const float r = cfg->smoothing_radius, r2 = r * r;
+  const uint32_t N = cfg->particle_count;
+  const float vn = cfg->viscocity_kernel_norm;
+  const float px = pred[2 * i], py = pred[2 * i + 1];
+  const int32_t cx = orc_f32_to_i32((px + x_max) / r);
+  const int32_t cy = orc_f32_to_i32((py + y_max) / r);
+  float wx = 0.0f, wy = 0.0f;
+  for (int o = 0; o < 9; ++o) {
+    const uint32_t key = orc_cell_key(wrap_add(cx, GRID_OFF[o][0]), wrap_add(cy, GRID_OFF[o][1]), N);
+    for (uint32_t j = offsets[key]; j < N; ++j) {
+      if (lookup[2 * j] != key) break;
+      const uint32_t oi = lookup[2 * j + 1];
+      if (oi == i) continue;
+      const float dx = px - pred[2 * oi], dy = py - pred[2 * oi + 1];
+      const float sq = dx * dx + dy * dy;
+      if (sq > r2) continue;
+      const float dist = sqrtf(sq);
+      float k = 0.0f;
+      if (!(dist >= r)) {
+        const float v = r * r - dist * dist;
+        k = ((vn * v) * v) * v; /* :181-188 */
+      }
+      wx = wx + (nvx[oi] - qx) * k;
+      wy = wy + (nvy[oi] - qy) * k;
+    }
+  }
+  *wx_out = wx;
+  *wy_out = wy;
+}
+
+/* apply_viscocity_force (:413-417), update_particle_positions (:392-395), walls (:69-99). */
+static inline void sim_finish(const rps_config* cfg, float* x, float* y, float* vx, float* vy,
+                              uint32_t i, float qx, float qy, float wx, float wy) {
+  const float dt = cfg->fixed_delta_time;
+  qx = qx + (wx * cfg->viscocity_strength) * dt;
+  qy = qy + (wy * cfg->viscocity_strength) * dt;
+  float ox = x[i] + qx * dt;
+  float oy = y[i] + qy * dt;
+  wall(cfg, &ox, &oy, &qx, &qy);
+  x[i] = ox;
+  y[i] = oy;
+  vx[i] = qx;
+  vy[i] = qy;
 }
 
 /* simulation_step (wgsl:435-453): pressure (:256-334), viscosity (:336-384), Euler
@@ -753,13 +867,6 @@ void orc_sph_sim(const rps_config* cfg, float* x, float* y, float* vx, float* vy
                  const uint32_t* lookup, const uint32_t* offsets, const float* dens,
                  const float* pred, uint32_t n) {
   const float dt = cfg->fixed_delta_time;
-  const float x_max = cfg->screen_bounds[1], y_max = cfg->screen_bounds[3];
-  const float r = cfg->smoothing_radius, r2 = r * r;
-  const uint32_t N = cfg->particle_count;
-  const float td = cfg->target_density, pm = cfg->pressure_multiplier;
-  const float nm = cfg->near_density_multiplier;
-  const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
-  const float vn = cfg->viscocity_kernel_norm;
   float* svx = (float*)malloc(sizeof(float) * n);
   float* svy = (float*)malloc(sizeof(float) * n);
   memcpy(svx, vx, sizeof(float) * n);
@@ -768,83 +875,74 @@ void orc_sph_sim(const rps_config* cfg, float* x, float* y, float* vx, float* vy
    * snapshot, so the OpenMP build (bench cpu_baseline) equals the serial checker bit for bit. */
 #pragma omp parallel for schedule(dynamic, 1024)
   for (uint32_t i = 0; i < n; ++i) {
-    const float px = pred[2 * i], py = pred[2 * i + 1];
-    const int32_t cx = orc_f32_to_i32((px + x_max) / r);
-    const int32_t cy = orc_f32_to_i32((py + y_max) / r);
-    const float rho = dens[2 * i], rhon = dens[2 * i + 1];
-    const float P = (rho - td) * pm;
-    const float Pn = rhon * nm;
-    float fx = 0.0f, fy = 0.0f;
-    for (int o = 0; o < 9; ++o) {
-      const uint32_t key = orc_cell_key(wrap_add(cx, GRID_OFF[o][0]), wrap_add(cy, GRID_OFF[o][1]), N);
-      for (uint32_t j = offsets[key]; j < N; ++j) {
-        if (lookup[2 * j] != key) break;
-        const uint32_t oi = lookup[2 * j + 1];
-        if (oi == i) continue;
-        const float dx = pred[2 * oi] - px, dy = pred[2 * oi + 1] - py;
-        const float sq = dx * dx + dy * dy;
-        if (sq > r2) continue;
-        const float dist = sqrtf(sq);
-        float dirx, diry;
-        if (dist > 0.0001f) {
-          dirx = dx / dist;
-          diry = dy / dist;
-        } else {
-          dirx = 0.0f;
-          diry = 1.0f;
-        }
-        const float rj = dens[2 * oi], rnj = dens[2 * oi + 1];
-        const float Pj = (rj - td) * pm;
-        const float Pnj = rnj * nm;
-        const float pt = (P / (rho * rho)) + (Pj / (rj * rj));
-        const float npt = (Pn / (rho * rho)) + (Pnj / (rj * rnj));
-        float dk = 0.0f, ndk = 0.0f;
-        if (!(dist >= r)) {
-          const float v = r - dist;
-          dk = (-2.0f * dn) * v;         /* :154-161 */
-          ndk = ((-3.0f * ndn) * v) * v; /* :172-179 */
-        }
-        fx = fx + (dirx * pt) * dk;
-        fy = fy + (diry * pt) * dk;
-        fx = fx + (dirx * npt) * ndk;
-        fy = fy + (diry * npt) * ndk;
-      }
-    }
-    /* apply_pressure_force (:407-411) */
-    float qx = vx[i] + fx * dt;
-    float qy = vy[i] + fy * dt;
-    /* calculate_viscocity (:336-384) */
-    float wx = 0.0f, wy = 0.0f;
-    for (int o = 0; o < 9; ++o) {
-      const uint32_t key = orc_cell_key(wrap_add(cx, GRID_OFF[o][0]), wrap_add(cy, GRID_OFF[o][1]), N);
-      for (uint32_t j = offsets[key]; j < N; ++j) {
-        if (lookup[2 * j] != key) break;
-        const uint32_t oi = lookup[2 * j + 1];
-        if (oi == i) continue;
-        const float dx = px - pred[2 * oi], dy = py - pred[2 * oi + 1];
-        const float sq = dx * dx + dy * dy;
-        if (sq > r2) continue;
-        const float dist = sqrtf(sq);
-        float k = 0.0f;
-        if (!(dist >= r)) {
-          const float v = r * r - dist * dist;
-          k = ((vn * v) * v) * v; /* :181-188 */
-        }
-        wx = wx + (svx[oi] - qx) * k;
-        wy = wy + (svy[oi] - qy) * k;
-      }
-    }
-    /* apply_viscocity_force (:413-417) */
-    qx = qx + (wx * cfg->viscocity_strength) * dt;
-    qy = qy + (wy * cfg->viscocity_strength) * dt;
-    float ox = x[i] + qx * dt;
-    float oy = y[i] + qy * dt;
-    wall(cfg, &ox, &oy, &qx, &qy);
-    x[i] = ox;
-    y[i] = oy;
-    vx[i] = qx;
-    vy[i] = qy;
+    float fx, fy, wx, wy;
+    pressure_one(cfg, lookup, offsets, dens, pred, i, &fx, &fy);
+    const float qx = svx[i] + fx * dt; /* apply_pressure_force (:407-411) */
+    const float qy = svy[i] + fy * dt;
+    viscosity_one(cfg, lookup, offsets, pred, svx, svy, i, qx, qy, &wx, &wy);
+    sim_finish(cfg, x, y, vx, vy, i, qx, qy, wx, wy);
   }
   free(svx);
   free(svy);
+}
+
+/* ----------------------------------------------------------------------------------- */
+/* Other legal WGSL schedules of passes 4-5 (test infrastructure: the spread of outputs a   */
+/* conforming WGSL implementation may produce; tools/wgsl_schedule_envelope.py).            */
+/* ----------------------------------------------------------------------------------- */
+/* The reference reads buffers that the same dispatch writes: calculate_density reads other
+ * invocations' predicted_positions (wgsl:240) while they are written (:430), and
+ * calculate_viscocity reads other particles' velocity (:371) while apply_pressure_force /
+ * apply_viscocity_force / check_screen_bounds write it (:410, :416, :452).  WGSL orders none
+ * of it.  These restatements execute invocation groups of `group` consecutive invocations one
+ * group after another in the order `order[0 .. ceil(n / group))`, each group in lockstep (every
+ * member finishes a statement before any member starts the next, as a wave does).  A group then
+ * reads its own and the earlier groups' writes and the previous contents for later groups: the
+ * previous frame's predicted positions, the start-of-pass velocities.  One group of all n
+ * invocations gives orc_sph_pre's bits, and a sim whose neighbours' velocities are post-pressure
+ * (the snapshot semantics of orc_sph_sim, start-of-pass velocities for every neighbour, is the
+ * weak-memory execution in which no write is seen before the pass ends); groups of one in
+ * index order are a serial CPU executor's schedule. */
+void orc_sph_pre_sched(const rps_config* cfg, float* vx, float* vy, const float* x,
+                       const float* y, const uint32_t* lookup, const uint32_t* offsets,
+                       float* dens, float* pred, uint32_t n, const uint32_t* order,
+                       uint32_t group) {
+  const uint32_t ng = (n + group - 1u) / group;
+  for (uint32_t k = 0; k < ng; ++k) {
+    const uint32_t lo = order[k] * group, hi = lo + group < n ? lo + group : n;
+    for (uint32_t i = lo; i < hi; ++i) predict_one(cfg, vx, vy, x, y, pred, i);
+    for (uint32_t i = lo; i < hi; ++i) density_one(cfg, lookup, offsets, pred, pred, i, &dens[2 * i], &dens[2 * i + 1]);
+  }
+}
+
+/* The weak-memory extreme of pass 4: no invocation sees another's new prediction (each
+ * density reads the other particles' predicted positions of the previous frame, pred_prev; its
+ * own is program-ordered, fresh).  Legal where the writes of other workgroups are not yet
+ * visible (non-coherent caches). */
+void orc_sph_pre_stale(const rps_config* cfg, float* vx, float* vy, const float* x, const float* y,
+                       const uint32_t* lookup, const uint32_t* offsets, float* dens, float* pred,
+                       const float* pred_prev, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i) predict_one(cfg, vx, vy, x, y, pred, i);
+  for (uint32_t i = 0; i < n; ++i) density_one(cfg, lookup, offsets, pred, pred_prev, i, &dens[2 * i], &dens[2 * i + 1]);
+}
+
+void orc_sph_sim_sched(const rps_config* cfg, float* x, float* y, float* vx, float* vy,
+                       const uint32_t* lookup, const uint32_t* offsets, const float* dens,
+                       const float* pred, uint32_t n, const uint32_t* order, uint32_t group) {
+  const float dt = cfg->fixed_delta_time;
+  const uint32_t ng = (n + group - 1u) / group;
+  float* w = (float*)malloc(sizeof(float) * 2u * (group < n ? group : n));
+  for (uint32_t k = 0; k < ng; ++k) {
+    const uint32_t lo = order[k] * group, hi = lo + group < n ? lo + group : n;
+    for (uint32_t i = lo; i < hi; ++i) { /* apply_pressure_force: velocity written in place */
+      float fx, fy;
+      pressure_one(cfg, lookup, offsets, dens, pred, i, &fx, &fy);
+      vx[i] = vx[i] + fx * dt;
+      vy[i] = vy[i] + fy * dt;
+    }
+    for (uint32_t i = lo; i < hi; ++i) /* calculate_viscocity: every member reads before any writes */
+      viscosity_one(cfg, lookup, offsets, pred, vx, vy, i, vx[i], vy[i], &w[2 * (i - lo)], &w[2 * (i - lo) + 1]);
+    for (uint32_t i = lo; i < hi; ++i) sim_finish(cfg, x, y, vx, vy, i, vx[i], vy[i], w[2 * (i - lo)], w[2 * (i - lo) + 1]);
+  }
+  free(w);
 }

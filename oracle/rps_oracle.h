@@ -105,6 +105,19 @@ void orc_sph_pre(const rps_config* cfg, float* vx, float* vy, const float* x, co
 void orc_sph_sim(const rps_config* cfg, float* x, float* y, float* vx, float* vy,
                  const uint32_t* lookup, const uint32_t* offsets, const float* dens,
                  const float* pred, uint32_t n);
+/* Passes 4-5 under another legal WGSL schedule: groups of `group` invocations in lockstep,
+ * executed one after another in the order order[0 .. ceil(n / group)) (rps_oracle.c). */
+void orc_sph_pre_sched(const rps_config* cfg, float* vx, float* vy, const float* x,
+                       const float* y, const uint32_t* lookup, const uint32_t* offsets,
+                       float* dens, float* pred, uint32_t n, const uint32_t* order,
+                       uint32_t group);
+void orc_sph_sim_sched(const rps_config* cfg, float* x, float* y, float* vx, float* vy,
+                       const uint32_t* lookup, const uint32_t* offsets, const float* dens,
+                       const float* pred, uint32_t n, const uint32_t* order, uint32_t group);
+/* Pass 4 with every other particle's prediction of the previous frame (pred_prev). */
+void orc_sph_pre_stale(const rps_config* cfg, float* vx, float* vy, const float* x, const float* y,
+                       const uint32_t* lookup, const uint32_t* offsets, float* dens, float* pred,
+                       const float* pred_prev, uint32_t n);
 
 #ifdef __cplusplus
 }

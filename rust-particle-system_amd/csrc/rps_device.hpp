@@ -288,15 +288,15 @@ __device__ __forceinline__ f4 set_color(float vx, float vy, float max_energy) {
   float nrm = energy / max_energy;
   nrm = nrm < 0.0f ? 0.0f : nrm;
   nrm = nrm > 1.0f ? 1.0f : nrm;
-  f4 rgba;
-  if (nrm < 0.5f) {
-    const float t = nrm * 2.0f;
-    rgba = f4{0.0f, t, 1.0f - t, 1.0f};
-  } else {
-    const float t = (nrm - 0.5f) * 2.0f;
-    rgba = f4{t, 1.0f - t, 0.0f, 1.0f};
-  }
-  return rgba;
+  // rgb = mix(a, b, t) = a * (1 - t) + b * t per component, as WGSL defines it (no constant
+  // folding: -fno-fast-math keeps 0 * t, so a NaN velocity colours NaN in every component, as
+  // the shader does; for finite t the literal form has the bits of t / 1 - t / 0).
+  const bool lo = nrm < 0.5f;
+  const float t = lo ? nrm * 2.0f : (nrm - 0.5f) * 2.0f;
+  const float a0 = 0.0f, a1 = lo ? 0.0f : 1.0f, a2 = lo ? 1.0f : 0.0f;  // blue -> green / green -> red
+  const float b0 = lo ? 0.0f : 1.0f, b1 = lo ? 1.0f : 0.0f, b2 = 0.0f;
+  const float u = 1.0f - t;
+  return f4{a0 * u + b0 * t, a1 * u + b1 * t, a2 * u + b2 * t, 1.0f};
 }
 
 // hash_cell + get_key_from_hash, compute_shader.wgsl:132-142 (u32 wrap).

@@ -43,11 +43,17 @@ def blob(n, seed):
                 vx=g.normal(0, 30, n).astype(F), vy=g.normal(0, 30, n).astype(F))
 
 
-def case(name, cfg, soa, frames):
+def case(name, cfg, soa, frames, schedules=None):
+    """schedules: {frame: (pre, sim)} -- frames run under the interpreter's other schedules
+    (stored as sched_pre / sched_sim per frame: 0 lockstep, 1 isolated)."""
     if ONLY and name not in ONLY:
         return
-    out = H.run_reference(cfg, soa, frames)
+    out = H.run_reference(cfg, soa, frames, schedules=schedules)
     d = dict(cfg=raw(cfg), frames=np.array([frames]))
+    code = {"lockstep": 0, "isolated": 1}
+    sch = [(schedules or {}).get(f, ("lockstep", "isolated")) for f in range(1, frames + 1)]
+    d["sched_pre"] = np.array([code[a] for a, _ in sch], np.uint8)
+    d["sched_sim"] = np.array([code[b] for _, b in sch], np.uint8)
     for k in ("x", "y", "vx", "vy"):
         d["in_" + k] = soa[k]
     for f, buf in enumerate(out, start=1):
@@ -93,6 +99,15 @@ def main():
         soa["x"] *= F(0.2)
         soa["y"] *= F(0.2)
         case(f"wgsl_sph_n{n}_tiny.npz", rps.default_particle_config(n, gravity=100.0), soa, 7)
+    # The shader's other legal outcomes of its intra-dispatch races: frames
+    # whose pass 4 runs "isolated" (every density reads the other particles' predictions of the
+    # previous frame) and / or pass 5 "lockstep" (the viscosity scan sees the neighbours'
+    # post-pressure velocities).  The oracle's schedule restatements (orc_sph_pre_stale,
+    # orc_sph_sim_sched with one group) must reproduce them; tools/wgsl_schedule_envelope.py
+    # measures how far these outcomes lie from the oracle's at larger N.
+    sched = {5: ("isolated", "isolated"), 6: ("lockstep", "lockstep"), 7: ("isolated", "lockstep")}
+    case("wgsl_sph_n64_sched.npz", rps.default_particle_config(64, gravity=100.0), blob(64, 5), 8, sched)
+    case("wgsl_sph_n100_sched.npz", rps.default_particle_config(100, gravity=100.0), blob(100, 6), 8, sched)
     # The streaming reference subset (C1): pressure, near-pressure and viscosity multipliers
     # zero, so each active frame is gravity -> Euler -> walls -> colour; particles on and
     # beyond the walls.

@@ -12,6 +12,8 @@ WGSL_SPH = ("wgsl_sph_n1_tiny.npz", "wgsl_sph_n2_tiny.npz", "wgsl_sph_n3_tiny.np
             "wgsl_sph_n64.npz", "wgsl_sph_n100.npz", "wgsl_sph_n512_default.npz", "wgsl_sph_n200_outside.npz",
             "wgsl_sph_n100_nan.npz")
 WGSL_STREAM = ("wgsl_stream_c1_n128.npz",)
+# The same shader with frames run under its other legal race outcomes (sched_pre / sched_sim):
+WGSL_SPH_SCHED = ("wgsl_sph_n64_sched.npz", "wgsl_sph_n100_sched.npz")
 
 
 def load(name):

@@ -422,6 +422,37 @@ def test_beyond_2pow32_particles(gpu, orc):
         assert_soa_bitwise(a, b, keys=KEYS_STEPS, what=f"chunk@{s} ")
 
 
+def test_colour_follows_wgsl_mix(gpu, orc):
+    """set_color (wgsl:101-118) colours by mix(a, b, t) = a * (1 - t) + b * t: a NaN speed makes
+    all three components NaN (0 * NaN included), as the shader's fixtures show
+    (tests/golden/wgsl_sph_n100_sched.npz); finite speeds give exactly t / 1 - t / 0.  Download
+    and device export against the oracle, bitwise, over rest, both branches, the 0.5 edge,
+    clamping, infinities and NaNs."""
+    from hip_mem import DeviceBuffer
+
+    rps = gpu
+    cfg = config_c1(rps, 16, gravity=0.0)
+    e = float(np.sqrt(2.0 * cfg.max_energy))  # |v| at energy = max_energy
+    vel = np.array([[0, 0], [e / 4, 0], [e / 2, 0], [0, e * np.sqrt(0.5)], [e, 0], [2 * e, 0], [np.inf, 0],
+                    [-np.inf, 1], [np.nan, 0], [0, np.nan], [np.nan, np.nan], [-e / 3, e / 5], [1e-30, 0],
+                    [-0.0, -0.0], [3.0, -4.0], [e * 0.75, 0]], F)
+    n = len(vel)
+    parts = np.zeros(n, rps.PARTICLE_DTYPE)
+    parts["velocity"] = vel
+    with rps.Context(n) as ctx, DeviceBuffer(n * 32) as buf:
+        ctx.set_config(cfg, rps.make_ext(shader_delay=0))
+        ctx.upload(parts)
+        ctx.step(1)  # an active step (set_color runs from the first one): no gravity, walls may flip v
+        got = ctx.download()
+        ctx.export_particles(buf.ptr.value)
+        exp = buf.to_host(rps.PARTICLE_DTYPE)
+    v = got["velocity"]
+    want = orc.set_color_array(v[:, 0], v[:, 1], cfg.max_energy)
+    assert np.isnan(want[8:11, :3]).all() and want[0].tolist() == [0.0, 0.0, 1.0, 1.0]
+    assert_bitwise(got["color"].reshape(-1), want.reshape(-1), "download colour")
+    assert_bitwise(exp["color"].reshape(-1), want.reshape(-1), "export colour")
+
+
 def test_render_export_matches_download(gpu):
     """rps_export_particles writes the reference's 32-B Particle buffer (position, velocity,
     derived colour) straight into device memory (render interop)."""

@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 import wgsl_harness as H
-from golden_io import WGSL_SPH, WGSL_STREAM, inputs, load, wgsl_config
+from golden_io import WGSL_SPH, WGSL_SPH_SCHED, WGSL_STREAM, inputs, load, wgsl_config
 from helpers import assert_bitwise, copy_soa
 
 
@@ -38,6 +38,39 @@ def test_oracle_sph_matches_reference_shader(rps, orc, name):
     for f in range(1, int(g["frames"][0]) + 1):
         fc, _ = orc.run_steps(2, cfg, ext, soa, 1, frame_count=fc, sph=st)
         _check_frame(g, f, soa, orc, cfg, st)
+
+
+@pytest.mark.parametrize("name", WGSL_SPH_SCHED)
+def test_oracle_schedule_restatements_match_reference_shader(rps, orc, name):
+    """The shader's other legal outcomes of its intra-dispatch races, as the interpreter runs
+    them (tests/golden/make_wgsl_golden.py): a frame whose pass 4 is "isolated" (each density
+    reads the other particles' predictions of the previous frame, the oracle's
+    orc_sph_pre_stale) and / or whose pass 5 is "lockstep" (the viscosity scan sees the
+    neighbours' post-pressure velocities: orc_sph_sim_sched with one group of all invocations).
+    Bitwise, frame by frame, with the default frames between them: the schedule restatements
+    behind tools/wgsl_schedule_envelope.py are the reference's own code's outcomes."""
+    g = load(name)
+    cfg, _ = wgsl_config(rps, g)
+    soa = inputs(g)
+    n = len(soa["x"])
+    st = orc.SphState(n)
+    seen = set()
+    for f in range(1, int(g["frames"][0]) + 1):
+        cfg.frame_count = f
+        st.grid(cfg, soa)
+        if f >= 5:  # SHADER_DELAY
+            pre, sim = int(g["sched_pre"][f - 1]), int(g["sched_sim"][f - 1])  # 0 lockstep, 1 isolated
+            seen.add((pre, sim))
+            if pre == 0:
+                st.pre(cfg, soa)
+            else:
+                st.pre_stale(cfg, soa)
+            if sim == 1:
+                st.sim(cfg, soa)
+            else:
+                st.sim_sched(cfg, soa, [0], n)
+        _check_frame(g, f, soa, orc, cfg, st)
+    assert {(1, 1), (0, 0), (1, 0), (0, 1)} <= seen
 
 
 @pytest.mark.parametrize("name", WGSL_STREAM)

@@ -14,6 +14,7 @@ Per frame, as `prepare_particle_buffers` (src/particle_buffers.rs:218-236) and
                                     density reads one: DESIGN.md §3.3)
   pass 5 simulation_step            isolated schedule (neighbour velocities from the pass's
                                     start, the particle's own post-pressure: DESIGN.md §3.3)
+  (other schedules per frame on request: the shader's other legal outcomes)
 Buffers start zero-filled, as wgpu's do; the lookup holds next_pow2(N) entries.
 """
 import os
@@ -70,7 +71,9 @@ class ReferenceSPH:
             "predicted_positions": W.Buffer([np.zeros(2, F32) for _ in range(n)]),
         }
 
-    def frame(self, cfg):
+    def frame(self, cfg, pre_schedule="lockstep", sim_schedule="isolated"):
+        """One frame.  The default schedules are the oracle's; the others give
+        the other legal outcomes of the shader's intra-dispatch races (tools/wgsl_schedule_envelope.py)."""
         n, P = self.n, self.P
         groups = lambda k: (k + WG - 1) // WG * WG
         uni = {"config": config_uniform(cfg), "sorting_params": None}
@@ -84,8 +87,8 @@ class ReferenceSPH:
                                          "step_index": U32(step)}
                 d.run("sort_particles", groups(P // 2))
         d.run("calculate_spatial_lookup_offsets", groups(n))
-        d.run("pre_simulation_step", groups(n), schedule="lockstep")
-        d.run("simulation_step", groups(n), schedule="isolated")
+        d.run("pre_simulation_step", groups(n), schedule=pre_schedule)
+        d.run("simulation_step", groups(n), schedule=sim_schedule)
 
     def arrays(self):
         b = self.buffers
@@ -101,8 +104,10 @@ class ReferenceSPH:
         }
 
 
-def run_reference(cfg, soa, frames, frame_count=0):
-    """`frames` frames of the reference over a copy of `soa`; per-frame buffer snapshots."""
+def run_reference(cfg, soa, frames, frame_count=0, schedules=None):
+    """`frames` frames of the reference over a copy of `soa`; per-frame buffer snapshots.
+    schedules: {frame index (1-based): (pre_schedule, sim_schedule)} for frames run under
+    other schedules than the oracle's."""
     import copy
 
     mod = load_module()
@@ -113,6 +118,6 @@ def run_reference(cfg, soa, frames, frame_count=0):
     for _ in range(frames):
         frame_count += 1
         c.frame_count = frame_count
-        ref.frame(c)
+        ref.frame(c, *((schedules or {}).get(frame_count, ("lockstep", "isolated"))))
         out.append(ref.arrays())
     return out
