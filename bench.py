@@ -402,6 +402,9 @@ def sph_roofline(cost, sim_ms, frame_ms, pmc):
     def frac(b, ms, peak):
         return rate(b, ms) / peak if b else None
 
+    # The sim's utilisation of the units that bound it (PMC counter pass of the same workload,
+    # tools/sph_counter_table.py): the texture addressers and the VALU, not bytes.
+    cnt = ((pmc or {}).get("counters", {}).get("per_kernel", {}) or {}).get(sim_name or "", {})
     hbm_frame = (pmc or {}).get("frame_sum_of_kernels", {}).get("hbm_bytes")
     l2_frame = (pmc or {}).get("frame_sum_of_kernels", {}).get("l2_bytes")
     sim_algo_gbps = cost["sim_bytes"] / (sim_ms * 1e-3) / 1e9
@@ -414,12 +417,16 @@ def sph_roofline(cost, sim_ms, frame_ms, pmc):
                 "algorithmic_bytes_per_launch": cost["sim_bytes"],
                 "algorithmic_equiv_gbps": sim_algo_gbps,
                 "algorithmic_equiv_frac": sim_algo_gbps / L2_PEAK_GBPS,
+                "ta_busy": cnt.get("ta_busy"), "valu_busy": cnt.get("valu_busy"), "l1_hit": cnt.get("l1_hit"),
+                "lines_per_load": cnt.get("lines_per_load"),
                 "scanned_entries_per_particle": cost["scanned_entries"] / cost["slots"],
                 "within_radius_per_particle": cost["within_entries"] / cost["slots"],
                 "note": "achieved/frac: the sim kernel's L1 -> L2 request bytes measured by the PMC counters "
                         "(traffic, per launch) / this run's kernel time, against the aggregate L2 peak; "
                         "hbm_frac: its memory-side bytes against HBM; algorithmic_equiv_*: every neighbour "
-                        "gather charged (mostly L1 hits) -- an equivalence, not a utilisation"}
+                        "gather charged (mostly L1 hits) -- an equivalence, not a utilisation; ta_busy / valu_busy: "
+                        "the units that bound the scan (texture addressers at ~29 cache lines per gather "
+                        "instruction, and the VALU), from the committed counter pass (DESIGN.md App. B)"}
     frame_cost = {"hbm_bytes_measured": hbm_frame, "hbm_bytes_source": pmc_src,
                   "hbm_gbps": rate(hbm_frame, frame_ms), "frac": frac(hbm_frame, frame_ms, HBM_PEAK_GBPS),
                   "bound": "hbm", "peak": HBM_PEAK_GBPS,

@@ -74,6 +74,8 @@ def main(tag):
         json.dump(doc, f, indent=1, sort_keys=True)
     path = os.path.join(PROF, "pmc_traffic.json")
     old = json.load(open(path)) if os.path.exists(path) else {}
+    if "counters" in old.get("SPH-2^22-frame", {}):  # tools/sph_counter_table.py --merge keeps its rows here
+        doc["counters"] = old["SPH-2^22-frame"]["counters"]
     old["SPH-2^22-frame"] = doc
     with open(path, "w") as f:
         json.dump(old, f, indent=1, sort_keys=True)

@@ -1,6 +1,9 @@
 """DESIGN.md §5.2's per-kernel counter table of the SPH frame, from tools/pmc_sph_counters.sh.
 
-    python tools/sph_counter_table.py [N] > profiles/<tag>_sph_counters_2p22.txt
+    python tools/sph_counter_table.py [N] [--merge TAG] > profiles/<tag>_sph_counters_2p22.txt
+
+--merge TAG also stores each kernel's row under "counters" in profiles/pmc_traffic.json's
+"SPH-2^22-frame" entry (bench.py's sph.roofline reports the sim's), tagged with the round.
 
 Kernel times: the kernel trace of the same box (no counters collected in that run).  Per kernel
 (counters averaged over the dispatches):
@@ -41,7 +44,12 @@ def counters(d):
 
 
 def main():
-    n = sys.argv[1] if len(sys.argv) > 1 else "4194304"
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    merge = sys.argv[sys.argv.index("--merge") + 1] if "--merge" in sys.argv else None
+    if merge in args:
+        args.remove(merge)
+    n = args[0] if args else "4194304"
+    rows = {}
     times = {}
     for r in csv.DictReader(open(find(f"cnt_trace_{n}", "kernel_stats.csv"))):
         times[short(r["Name"])] = float(r["AverageNs"]) / 1e3
@@ -60,12 +68,27 @@ def main():
         acc = a.get("TCP_TOTAL_CACHE_ACCESSES_sum", 0.0)
         hit, miss = b.get("TCC_HIT_sum", 0.0), b.get("TCC_MISS_sum", 0.0)
         wc = b.get("SQ_WAVE_CYCLES", 0.0) or float("nan")
+        rows[k] = {"us": us, "lines_per_load": acc / vm if vm else None,
+                   "l1_hit": 1.0 - a.get("TCP_TCC_READ_REQ_sum", 0.0) / acc if acc else None,
+                   "l2_hit": hit / (hit + miss) if hit + miss else None,
+                   "ta_busy": a.get("TA_TA_BUSY_sum", 0.0) / CUS / cyc,
+                   "valu_busy": a.get("SQ_INSTS_VALU", 0.0) * 2.0 / SIMDS / cyc,
+                   "sq_wait": b.get("SQ_WAIT_ANY", 0.0) / wc, "sq_instwait": b.get("SQ_WAIT_INST_ANY", 0.0) / wc}
         print(f"{k[:44]:44} {us:7.1f} {acc / vm if vm else float('nan'):8.1f} "
               f"{1.0 - a.get('TCP_TCC_READ_REQ_sum', 0.0) / acc if acc else float('nan'):6.3f} "
               f"{hit / (hit + miss) if hit + miss else float('nan'):6.3f} "
               f"{a.get('TA_TA_BUSY_sum', 0.0) / CUS / cyc:6.2f} {a.get('SQ_INSTS_VALU', 0.0) * 2.0 / SIMDS / cyc:8.2f} "
               f"{b.get('SQ_WAIT_ANY', 0.0) / wc:5.2f} {b.get('SQ_WAIT_INST_ANY', 0.0) / wc:5.2f} "
               f"{b.get('SQ_ACTIVE_INST_VALU', 0.0) / wc:5.2f}")
+    if merge:
+        import json
+
+        path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        doc = json.load(open(path))
+        doc.setdefault("SPH-2^22-frame", {})["counters"] = {"round": merge, "per_kernel": rows,
+                                                            "source": "tools/pmc_sph_counters.sh + tools/sph_counter_table.py"}
+        with open(path, "w") as f:
+            json.dump(doc, f, indent=1, sort_keys=True)
 
 
 if __name__ == "__main__":
