@@ -71,7 +71,10 @@ def parse():
                     help="all-pairs CPU baseline size (SURVEY 8d: 65 536, every target x every source; 0: skip)")
     ap.add_argument("--sph-n", type=int, default=1 << 22,
                     help="particles of the SPH-frame side measurement per rank (0: skip)")
-    ap.add_argument("--sph-frames", type=int, default=50)
+    ap.add_argument("--sph-frames", type=int, default=200,
+                    help="timed SPH frames after --sph-warm untimed ones (the window every SPH timing here uses: "
+                         "the frame cost drifts with the frame index, DESIGN.md App. B)")
+    ap.add_argument("--sph-warm", type=int, default=20)
     ap.add_argument("--sph-cpu-n", type=int, default=1 << 22,
                     help="particles of the SPH CPU-baseline sample (oracle, OpenMP)")
     ap.add_argument("--sph-cpu-frames", type=int, default=3)
@@ -452,7 +455,7 @@ def sph_side(rps, args, d):
     try:
         ctx.set_config(cfg, rps.make_ext(shader_delay=0))
         ctx.upload(parts)
-        ctx.step(10)
+        ctx.step(args.sph_warm)
         ctx.sync()
         d.sync_device()
         d.barrier()
@@ -477,7 +480,7 @@ def sph_side(rps, args, d):
     spatial = layout == "2" or (layout == "1" and slots >= (1 << 20))  # rps_context.hip
     out = {"workload": f"SPH frame (5 passes, bitwise == oracle), {n} particles per rank, reference scatter",
            "record_layout": "cell tiles (spatial)" if spatial else "lookup order",
-           "scaling": "replicas", "frames": args.sph_frames, "ms_per_frame": frame_ms,
+           "scaling": "replicas", "warm_frames": args.sph_warm, "frames": args.sph_frames, "ms_per_frame": frame_ms,
            "particle_steps_per_s": float(n) * d.world * args.sph_frames / el,
            "sim_kernel_ms": sim_ms, "roofline": rl, "frame_cost": fc}
     out["reference_sizes"] = [sph_small(rps, args, d, m) for m in (50000, 65536)]
@@ -494,19 +497,20 @@ def sph_small(rps, args, d, n):
     count for the same network (the frame's other kernels: DESIGN.md §5.2)."""
     cfg = rps.default_particle_config(n)
     parts = rps.setup_particles_scatter(cfg, n, seed=args.seed)
-    frames = 200
+    frames = args.sph_frames
     ctx = rps.Context(n, rps.MODE_SPH, device=d.local if d.dist else 0)
     try:
         ctx.set_config(cfg, rps.make_ext(shader_delay=0))
         ctx.upload(parts)
-        ctx.step(20)
+        ctx.step(args.sph_warm)
         ctx.sync()
         ms = ctx.time_steps(frames) / frames
         cost = ctx.sph_frame_cost()
     finally:
         ctx.close()
     s = max(0, (n - 1).bit_length())
-    return {"particles": n, "frames": frames, "ms_per_frame": d.max(ms), "sort_launches": cost["sort_launches"],
+    return {"particles": n, "warm_frames": args.sph_warm, "frames": frames, "ms_per_frame": d.max(ms),
+            "sort_launches": cost["sort_launches"],
             "reference_dispatches_per_frame": 4 + s * (s + 1) // 2,
             "timing": "one HIP event pair around the frames on the context stream (rps_time_steps), every frame active"}
 
