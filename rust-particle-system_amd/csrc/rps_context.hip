@@ -58,7 +58,6 @@ struct rps_ctx {
   uint8_t csort_wide = 4; // RPS_SPH_CSORT_WIDE
   uint32_t pair_max_p = 0; // RPS_SPH_PAIRS: lane-pair scans up to this P
   bool sim_fuse = true;    // RPS_SPH_SIM_FUSE: the sim and its long scans in one launch
-  uint8_t sim_flat = 0;    // RPS_SPH_SIM_FLAT: the flattened (slot, entry) sim scans (1: 128, 2: 256 pairs per round)
   uint8_t lane_group = 2;  // RPS_SPH_GROUP: lanes per slot of the small-P scans (2 or 4)
   uint8_t lane_group_s = 2;  // RPS_SPH_GROUP_S: the sim's (default: lane_group)
   uint8_t sph_batch_d = 0, sph_batch_s = 0;  // forced scan batches (0: by size)
@@ -325,7 +324,6 @@ SphBuffers sph_buffers(rps_ctx* ctx) {
   b.csort_wide = ctx->csort_wide;
   b.pair_max_p = ctx->pair_max_p;
   b.sim_fuse = ctx->sim_fuse;
-  b.sim_flat = ctx->sim_flat;
   b.lane_group = ctx->lane_group;
   b.lane_group_s = ctx->lane_group_s;
   return b;
@@ -671,7 +669,6 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     ctx->csort_wide = (uint8_t)std::max(0, std::min(5, env_int("RPS_SPH_CSORT_WIDE", 4)));
     ctx->pair_max_p = (uint32_t)std::max(0, env_int("RPS_SPH_PAIRS", 1 << 17));
     ctx->sim_fuse = env_int("RPS_SPH_SIM_FUSE", 1) != 0;
-    ctx->sim_flat = (uint8_t)std::min(2, std::max(0, env_int("RPS_SPH_SIM_FLAT", 0)));
     // Lanes per slot of the small-P scans: 4 below 65 536 particles (same box, ms/frame: 20 000
     // 0.0561 -> 0.0531, 50 000 0.0883 -> 0.0863), 2 from there (65 536 0.0761 / 0.0769 with 4,
     // 100 000 0.1215 / 0.1307); RPS_SPH_GROUP=2 or 4 forces one.

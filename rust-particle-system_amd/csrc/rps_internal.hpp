@@ -189,7 +189,6 @@ struct SphBuffers {
   uint8_t csort_wide;  // its stages of this many folded passes or more fold with twice the threads (0: none), RPS_SPH_CSORT_WIDE
   uint32_t pair_max_p;  // P <= this: density / sim scans by lane pairs (RPS_SPH_PAIRS)
   bool sim_fuse;        // P != N: the sim and its long scans in one launch (RPS_SPH_SIM_FUSE)
-  uint8_t sim_flat;     // P == N: the flattened (slot, entry) sim, 1: 128 / 2: 256 pairs per round (RPS_SPH_SIM_FLAT)
   uint8_t lane_group;   // lanes per slot of those scans: 2 or 4 (RPS_SPH_GROUP)
   uint8_t lane_group_s; // the same for the sim's scans (RPS_SPH_GROUP_S; default: lane_group)
   uint32_t cell_cap; // capacity of lay.cell_info / cellrun (0: layout never available)

@@ -2583,168 +2583,6 @@ __global__ __launch_bounds__(kBlock) void sph_sim_kernel(const rps_config* __res
   sim_body<kScanBatch, kPads, LAYOUT>(cfg, rb, sl, st, bin_next, p_slots, blockIdx.x, runs);
 }
 
-// Flattened (slot, entry) sim scans (P == N; RPS_SPH_SIM_FLAT):
-// a wave deals the set bits of its 64 lanes' masks -- every (slot, within-radius entry) pair
-// -- evenly over its lanes instead of each lane walking its own bits, so a wave waits for the
-// mean list, not the longest.  Rounds of CAP pairs: (1) each owner lane writes its pairs
-// falling in the round, (entry slot << 6 | owner lane), to the wave's pair buffer, walking
-// its own bits in order with its run cursor; (2) every lane takes CAP / 64 pairs, gathers the
-// entry's record and evaluates the owner's term (the owner's loop invariants from LDS),
-// writing it to the wave's term buffer; (3) every owner adds its round's terms from the
-// buffer in its own bit order (the reference's order; self skipped).  The same additions in
-// the same order as sph_sim_kernel, so the same bits.  Lanes whose nine runs hold more than
-// 128 entries (no mask) scan their runs as sph_sim_kernel does.
-template <uint32_t CAP, class T, class TermFn, class AddFn>
-__device__ __forceinline__ void flat_scan(const RunTable& runs, uint64_t m0, uint64_t m1, uint32_t self,
-                                          uint32_t* __restrict__ pairs, T* __restrict__ terms, TermFn&& term,
-                                          AddFn&& add) {
-  static_assert(CAP % 64 == 0, "whole chunks of 64 pairs");
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t c = (uint32_t)(__builtin_popcountll(m0) + __builtin_popcountll(m1));
-  uint32_t incl = c;  // inclusive prefix of the lanes' pair counts
-#pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint32_t y = (uint32_t)__shfl_up((int)incl, d, 64);
-    if (lane >= d) incl += y;
-  }
-  const uint32_t W = (uint32_t)__shfl((int)incl, 63, 64);
-  const uint32_t base = incl - c;
-  uint32_t r = 0, done = 0;
-  uint2 cur = runs[0][threadIdx.x];
-  for (uint32_t R = 0; R < W; R += CAP) {
-    while (done < c && base + done < R + CAP) {  // (1) my pairs of this round, in bit order
-      uint32_t f;
-      if (m0) {
-        f = (uint32_t)__builtin_ctzll(m0);
-        m0 &= m0 - 1u;
-      } else {
-        f = 64u + (uint32_t)__builtin_ctzll(m1);
-        m1 &= m1 - 1u;
-      }
-      while (f >= cur.y) cur = runs[++r][threadIdx.x];
-      pairs[base + done - R] = ((f + cur.x) << 6) | lane;
-      ++done;
-    }
-    wave_lds_sync();
-    const uint32_t cnt = W - R < CAP ? W - R : CAP;
-    term(pairs, terms, cnt);  // (2) CAP / 64 pairs per lane, terms into the buffer
-    wave_lds_sync();
-    const uint32_t lo = base > R ? base : R, hi = base + c < R + cnt ? base + c : R + cnt;
-    for (uint32_t k = lo; k < hi; ++k)  // (3) my terms of this round, in my bit order
-      if ((pairs[k - R] >> 6) != self) add(terms[k - R]);
-    wave_lds_sync();
-  }
-}
-
-template <uint32_t CAP, bool LAYOUT>
-__global__ __launch_bounds__(kBlock) void sph_sim_flat_kernel(const rps_config* __restrict__ cfg, RunBounds rb,
-                                                              SphSlots sl, f4* __restrict__ st,
-                                                              uint2* __restrict__ bin_next, uint32_t p_slots) {
-  __shared__ RunTable runs;
-  __shared__ uint32_t pairs_w[kBlock / 64][CAP];
-  __shared__ f4 terms_w[kBlock / 64][CAP];  // pressure: 4 terms; viscosity: 2 (the same bytes)
-  __shared__ f4 own_w[kBlock];               // the owners' loop invariants, by lane
-  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-  const bool in = t < p_slots;  // every lane of a wave stays: the scans are wave-wide
-  const uint32_t wv = threadIdx.x >> 6, wbase = threadIdx.x & ~63u;
-  uint32_t* const pairs = pairs_w[wv];
-  f4* const terms = terms_w[wv];
-  const float dt = cfg->fixed_delta_time;
-  const float r = cfg->smoothing_radius, r2 = r * r;
-  const uint32_t N = cfg->particle_count;
-  const float dn = cfg->density_kernel_norm, ndn = cfg->near_density_kernel_norm;
-  const float vn = cfg->viscocity_kernel_norm;
-  const SimOwn o = in ? sim_own(cfg, sl, t) : SimOwn{f2{0.0f, 0.0f}, 0.0f, 0.0f, 0u};
-  const f2 p = o.p;
-  uint32_t total = 0;
-  if (in) {
-    total = nine_runs<LAYOUT>(rb, p[0], p[1], cfg->screen_bounds[1], cfg->screen_bounds[3], r, N, runs);
-  } else {
-    runs[0][threadIdx.x] = make_uint2(0u, 0u);
-  }
-  const bool masked = in && total <= 128u;
-  const uint64_t m0 = masked ? __builtin_nontemporal_load(sl.nbr_mask + t) : 0u,
-                 m1 = masked ? __builtin_nontemporal_load(sl.nbr_mask + p_slots + t) : 0u;
-  const uint32_t self = t;
-  float fx = 0.0f, fy = 0.0f;
-  own_w[threadIdx.x] = f4{p[0], p[1], o.P_rho2, o.Pn_rho2};
-  const auto pressure_terms_of = [&](const uint32_t* pr, f4* tm, uint32_t cnt) {
-    constexpr int U = CAP / 64;
-    uint32_t pk[U];
-    f4 q[U], ow[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t k = (threadIdx.x & 63u) + 64u * u;
-      pk[u] = k < cnt ? pr[k] : (threadIdx.x & 63u);  // an idle pair: slot 0, a valid address
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      q[u] = sl.rec_pd[pk[u] >> 6];
-      ow[u] = own_w[wbase + (pk[u] & 63u)];
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t k = (threadIdx.x & 63u) + 64u * u;
-      const f4 w = pressure_terms(q[u], f2{ow[u][0], ow[u][1]}, ow[u][2], ow[u][3], r, dn, ndn);
-      if (k < cnt) tm[k] = w;
-    }
-  };
-  const auto pressure_add = [&](const f4& w) {
-    fx = fx + w[0];
-    fy = fy + w[1];
-    fx = fx + w[2];
-    fy = fy + w[3];
-  };
-  flat_scan<CAP, f4>(runs, m0, m1, self, pairs, terms, pressure_terms_of, pressure_add);
-  const auto load_pd = [&](uint32_t j) { return sl.rec_pd[j]; };
-  const auto pressure = [&](const f4& q) { pressure_add(pressure_terms(q, p, o.P_rho2, o.Pn_rho2, r, dn, ndn)); };
-  const auto pressure_nan = [&] { return fx != fx && fy != fy; };
-  if (in && !masked) scan_runs<4, false>(sl, runs, 0u, total, p, r2, self, load_pd, pressure, pressure_nan);
-  const f4 own_pv = in ? sl.rec_pv[t] : f4{0.0f, 0.0f, 0.0f, 0.0f};
-  const float qx = own_pv[2] + fx * dt;  // post-gravity velocity (the pre pass, wgsl:397-400)
-  const float qy = own_pv[3] + fy * dt;
-  float wx = 0.0f, wy = 0.0f;
-  wave_lds_sync();  // every lane of the wave is past its reads of own_w
-  own_w[threadIdx.x] = f4{p[0], p[1], qx, qy};
-  f2* const vterms = reinterpret_cast<f2*>(terms);
-  const auto viscosity_terms_of = [&](const uint32_t* pr, f2* tm, uint32_t cnt) {
-    constexpr int U = CAP / 64;
-    uint32_t pk[U];
-    f4 q[U], ow[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t k = (threadIdx.x & 63u) + 64u * u;
-      pk[u] = k < cnt ? pr[k] : (threadIdx.x & 63u);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      q[u] = sl.rec_pv[pk[u] >> 6];
-      ow[u] = own_w[wbase + (pk[u] & 63u)];
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t k = (threadIdx.x & 63u) + 64u * u;
-      const float kv = viscosity_weight(q[u], f2{ow[u][0], ow[u][1]}, r, vn);
-      const f2 w = {(q[u][2] - ow[u][2]) * kv, (q[u][3] - ow[u][3]) * kv};
-      if (k < cnt) tm[k] = w;
-    }
-  };
-  const auto viscosity_add = [&](const f2& w) {
-    wx = wx + w[0];
-    wy = wy + w[1];
-  };
-  flat_scan<CAP, f2>(runs, m0, m1, self, pairs, vterms, viscosity_terms_of, viscosity_add);
-  const auto load_pv = [&](uint32_t j) { return sl.rec_pv[j]; };
-  const auto viscosity = [&](const f4& q) {
-    const float k = viscosity_weight(q, p, r, vn);
-    wx = wx + (q[2] - qx) * k;
-    wy = wy + (q[3] - qy) * k;
-  };
-  const auto viscosity_nan = [&] { return wx != wx && wy != wy; };
-  if (in && !masked) scan_runs<4, false>(sl, runs, 0u, total, p, r2, self, load_pv, viscosity, viscosity_nan);
-  if (in) sim_finish<LAYOUT>(cfg, sl, st, bin_next, t, o.i, qx, qy, wx, wy);
-}
-
 // Lane-pair drivers of the sim's scans (see sph_density2_kernel): the entries split between the
 // lanes of a pair -- masked: the set bits alternately (the even lane the 1st, 3rd, ... of each
 // batch's pairs of bits); runs: flat entries f + 2u + par --, each lane evaluating its entries'
@@ -3993,20 +3831,6 @@ hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s) {
       if (b.batch_s == 4) { RPS_SIM2(4, 2); } else { RPS_SIM2(2, 2); }
     }
 #undef RPS_SIM2
-  } else if (b.sim_flat && b.p == b.n && b.p <= (1u << 26)) {  // entry slots fit the pair's 26 bits
-#define RPS_SIMFLAT(C)                                                                                          \
-  if (b.layout)                                                                                                 \
-    hipLaunchKernelGGL((sph_sim_flat_kernel<C, true>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg, rb,    \
-                       b.sl, b.st, b.bin_next, b.p);                                                            \
-  else                                                                                                          \
-    hipLaunchKernelGGL((sph_sim_flat_kernel<C, false>), dim3(blocks_for(b.p)), dim3(kBlock), 0, s, b.cfg, rb,   \
-                       b.sl, b.st, b.bin_next, b.p)
-    if (b.sim_flat == 1) {
-      RPS_SIMFLAT(128);
-    } else {
-      RPS_SIMFLAT(256);
-    }
-#undef RPS_SIMFLAT
   } else {
     switch (sph_batch(false, b.p, b.batch_s, b.layout)) {
       case 4: RPS_SIM(4); break;
