@@ -986,18 +986,28 @@ __device__ __forceinline__ void lds_chunk(uint2* lds, uint32_t t) {
   }
 }
 
-// The middle chunks: strides 2^LG down to 2^4, three passes per chunk (the last one fewer);
+// The middle chunks: strides 2^LG down to 2^LO, three passes per chunk (the last one fewer);
 // a chunk whose span 2G exceeds one wave's 512 entries ends with a workgroup barrier.
-template <int LG>
+template <int LG, int LO>
 __device__ __forceinline__ void lds_chunks(uint2* lds, uint32_t t) {
-  if constexpr (LG >= 4) {
-    constexpr int K = LG - 3 >= 3 ? 3 : LG - 3;
+  if constexpr (LG >= LO) {
+    constexpr int K = LG - LO + 1 >= 3 ? 3 : LG - LO + 1;
     lds_chunk<LG, K>(lds, t);
     if constexpr ((2 << LG) > 512) __syncthreads();
     else wave_lds_sync();
-    lds_chunks<LG - K>(lds, t);
+    lds_chunks<LG - K, LO>(lds, t);
   }
 }
+
+// Where the LDS chunks of a tile's in-tile passes stop (log2 of the last LDS stride); the passes
+// below run in registers.  Tiles of 8192 entries (16 waves): stride 8 as a DPP exchange across a
+// lane pair (tails) and strides 16, 8 across a lane quad (head), measured faster there; smaller
+// tiles: every stride down to 8 in LDS, so the lane keeps only 4, 2, 1 (2^20 head 20.0 -> 18.9 us,
+// 2^19 13.2 -> 12.6, profiles/r06_sort_stride8_ab.txt; at 2^22 the head went 55.9 -> 56.9).
+template <int TLOG>
+constexpr int kTailLdsLo = TLOG >= 13 ? 4 : 3;
+template <int TLOG>
+constexpr int kHeadLdsLo = TLOG >= 13 ? 5 : 3;
 
 // A pass across lanes: entry j of this lane against entry j (REV: 7 - j) of the DPP partner
 // (quad_perm CTRL); `left` = this lane holds the lower position of each pair.
@@ -1135,14 +1145,15 @@ __global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_e
     for (int j = 0; j < 8; ++j) lds[a + pad_off<NT>(j)] = v[j];
   }
   __syncthreads();
-  lds_chunks<TLOG - 4>(lds, t);
-  {  // strides 8, 4, 2, 1: lane pair (2k, 2k + 1) holds the 16 entries [16k, 16k + 16)
+  lds_chunks<TLOG - 4, kTailLdsLo<TLOG>>(lds, t);
+  {  // strides 8 (DPP across the lane pair (2k, 2k + 1), 8192-entry tiles), 4, 2, 1: the lane's
+     // eight consecutive entries [8t, 8t + 8)
     const uint32_t a = padded(8u * t);
     uint2 v[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] = lds[a + i];
-    xlane_pass<kDppXor1, false>(v, (t & 1u) == 0u);  // stride 8: entry i of the left lane vs the right's
-    group_passes<3>(v);  // strides 4, 2, 1 inside the lane's eight
+    if constexpr (kTailLdsLo<TLOG> > 3) xlane_pass<kDppXor1, false>(v, (t & 1u) == 0u);
+    group_passes<3>(v);
     store_eight<TLOG == 13>(tile, t, v);
   }
 }
@@ -1200,15 +1211,15 @@ __device__ __forceinline__ void lds_sync() {
   else wave_lds_sync();
 }
 
-// Non-flip strides 2^LG down to 32, register chunks of up to three passes; each chunk is
+// Non-flip strides 2^LG down to 2^LO, register chunks of up to three passes; each chunk is
 // followed by the sync its span needs (the register tail reads the lane's own entries next).
-template <int LG>
+template <int LG, int LO>
 __device__ __forceinline__ void lds_mid_chunks(uint2* lds, uint32_t t) {
-  if constexpr (LG >= 5) {
-    constexpr int K = LG - 4 >= 3 ? 3 : LG - 4;
+  if constexpr (LG >= LO) {
+    constexpr int K = LG - LO + 1 >= 3 ? 3 : LG - LO + 1;
     lds_chunk<LG, K>(lds, t);
     lds_sync<(2 << LG)>();
-    lds_mid_chunks<LG - K>(lds, t);
+    lds_mid_chunks<LG - K, LO>(lds, t);
   }
 }
 
@@ -1229,10 +1240,11 @@ __device__ __forceinline__ void head_stages(uint2* lds, uint32_t t, uint2 (&v)[8
     lds_sync<(2 << S)>();
     lds_flip_chunk<S>(lds, t);
     lds_sync<(2 << S)>();
-    lds_mid_chunks<S - 2>(lds, t);
+    lds_mid_chunks<S - 2, kHeadLdsLo<TLOG>>(lds, t);
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] = lds[a + i];
-    reg_tail<(S >= 6)>(v, t);
+    if constexpr (kHeadLdsLo<TLOG> > 3) reg_tail<(S >= 6)>(v, t);  // strides 16, 8 by DPP, then 4, 2, 1
+    else group_passes<3>(v);                                          // strides 4, 2, 1
     // The next stage's first LDS write goes to this lane's own entries, which only this
     // wave's chunks read in this stage once the last cross-wave chunk's barrier has passed.
     head_stages<S + 1, TLOG>(lds, t, v);

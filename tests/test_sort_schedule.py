@@ -112,15 +112,27 @@ def tail(tile, TLOG):
     group_passes(v, 3)
     lds = np.zeros_like(tile)
     lds[t[:, None] + np.arange(8)[None, :] * nt] = v
+    LO = tail_lds_lo(TLOG)
     LG = TLOG - 4
-    while LG >= 4:
-        K = 3 if LG - 3 >= 3 else LG - 3
+    while LG >= LO:
+        K = min(3, LG - LO + 1)
         lds_chunk(lds, nt, LG, K)
         LG -= K
     v = lds[8 * t[:, None] + np.arange(8)[None, :]].copy()
-    xlane(v, t ^ 1, False, (t & 1) == 0)
+    if LO > 3:
+        xlane(v, t ^ 1, False, (t & 1) == 0)
     group_passes(v, 3)
     return v.reshape(-1, 2)
+
+
+def tail_lds_lo(TLOG):
+    """kTailLdsLo<TLOG>: the last LDS stride's log2 (8192-entry tiles: stride 8 by DPP)."""
+    return 4 if TLOG >= 13 else 3
+
+
+def head_lds_lo(TLOG):
+    """kHeadLdsLo<TLOG>: the last LDS stride's log2 (8192-entry tiles: strides 16, 8 by DPP)."""
+    return 5 if TLOG >= 13 else 3
 
 
 def xstrides(v, t, LG):
@@ -249,15 +261,17 @@ def head(tile, TLOG):
         for i, j in ((0, 7), (1, 6), (4, 3), (5, 2), (0, 1), (2, 3), (4, 5), (6, 7)):  # lds_flip_chunk
             cas(w, i, j)
         lds[ia], lds[ib] = w[:, :4], w[:, 4:]
+        LO = head_lds_lo(TLOG)
         LG = S - 2
-        while LG >= 5:
-            K = 3 if LG - 4 >= 3 else LG - 4
+        while LG >= LO:
+            K = min(3, LG - LO + 1)
             lds_chunk(lds, nt, LG, K)
             LG -= K
         v = lds[own].copy()
-        if S >= 6:
-            xlane(v, t ^ 2, False, (t & 2) == 0)
-        xlane(v, t ^ 1, False, (t & 1) == 0)
+        if LO > 3:
+            if S >= 6:
+                xlane(v, t ^ 2, False, (t & 2) == 0)
+            xlane(v, t ^ 1, False, (t & 1) == 0)
         group_passes(v, 3)
     return v.reshape(-1, 2)
 
