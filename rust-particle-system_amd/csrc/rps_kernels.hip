@@ -1263,19 +1263,42 @@ __device__ __forceinline__ void bin_load(const uint2* lookup, const SortBin& bin
     raw[k] = gq >= bin.n ? lookup[gq] : bin.prebuilt ? bin.prebuilt[gq] : __builtin_bit_cast(uint2, bin_pos(bin, gq));
   }
 }
-template <uint32_t NT>
-__device__ __forceinline__ void bin_keys(const SortBin& bin, uint32_t base0, uint32_t t, const uint2 (&raw)[8],
-                                         const PaddedTile& s) {
+
+// The bin pass for the eight consecutive entries [g0, g0 + 8): the sim's prebuilt (key, slot)
+// entries and the pad entries [n, P) as four 16-B loads where the eight are all of one kind,
+// positions keyed otherwise; offsets reset as bin_particles_in_grid does (wgsl:467).
+__device__ __forceinline__ void bin_load_eight(const uint2* lookup, const SortBin& bin, uint32_t g0, uint2 (&v)[8]) {
+  const uint2* src = g0 >= bin.n ? lookup + g0 : bin.prebuilt && g0 + 8u <= bin.n ? bin.prebuilt + g0 : nullptr;
+  if (src) {
+    const uint4* q = reinterpret_cast<const uint4*>(src);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint4 w = q[i];
+      v[2 * i] = make_uint2(w.x, w.y);
+      v[2 * i + 1] = make_uint2(w.z, w.w);
+    }
+    if (g0 < bin.n && bin.reset_pre) {
+#pragma unroll
+      for (uint32_t k = 0; k < 8; ++k) bin_reset(bin, g0 + k);
+    }
+    return;
+  }
+  uint2 raw[8];
 #pragma unroll
   for (uint32_t k = 0; k < 8; ++k) {
-    const uint32_t q = t + k * NT, gq = base0 + q;
+    const uint32_t gq = g0 + k;
+    raw[k] = gq >= bin.n ? lookup[gq] : bin.prebuilt ? bin.prebuilt[gq] : __builtin_bit_cast(uint2, bin_pos(bin, gq));
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < 8; ++k) {
+    const uint32_t gq = g0 + k;
     if (gq >= bin.n) {
-      s[q] = raw[k];
-    } else if (bin.prebuilt) {  // (key, slot) of a layout frame: offsets are rebuilt on debug
-      if (bin.reset_pre) bin_reset(bin, gq);  // readback (rps_read_debug); the sim's (key, i) of a
-      s[q] = raw[k];                           // frame without layout: reset here
+      v[k] = raw[k];
+    } else if (bin.prebuilt) {
+      if (bin.reset_pre) bin_reset(bin, gq);
+      v[k] = raw[k];
     } else {
-      s[q] = bin_key(bin, __builtin_bit_cast(f2, raw[k]), gq);
+      v[k] = bin_key(bin, __builtin_bit_cast(f2, raw[k]), gq);
     }
   }
 }
@@ -1283,28 +1306,19 @@ __device__ __forceinline__ void bin_keys(const SortBin& bin, uint32_t base0, uin
 template <int TLOG>
 __global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_eu(4))) void sph_sort_head_kernel(uint2* __restrict__ lookup, SortBin bin) {
   static_assert(TLOG >= 10 && TLOG <= 13, "eight entries per thread, 128..1024 threads");
-  constexpr uint32_t TILE = 1u << TLOG, NT = TILE / 8;
+  constexpr uint32_t TILE = 1u << TLOG;
   __shared__ uint2 lds[TILE + TILE / 32];
-  const PaddedTile s{lds};
   const uint32_t t = threadIdx.x;
   const uint32_t base0 = blockIdx.x * TILE;
-  {  // bin: every position (or pad entry) load first, then the keys
-    uint2 raw[8];
-    bin_load<NT>(lookup, bin, base0, t, raw);
-    bin_keys<NT>(bin, base0, t, raw, s);
-  }
-  __syncthreads();
   uint2 v[8];
-  const uint32_t a = padded(8u * t);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) v[i] = lds[a + i];
+  // bin: the lane's eight consecutive entries [8t, 8t + 8) straight from memory (no LDS image:
+  // stages 0-4 run in registers), every load first, then the keys
+  bin_load_eight(lookup, bin, base0 + 8u * t, v);
   reg_stages012(v);
   xlane_pass<kDppXor1, true>(v, (t & 1u) == 0u);  // stage 3: flip G = 8 (lane pair), then 4, 2, 1
   group_passes<3>(v);
   xlane_pass<kDppRev4, true>(v, (t & 2u) == 0u);  // stage 4: flip G = 16 (lane quad), then 8 ... 1
   reg_tail<false>(v, t);
-  // The bin's LDS image was read back by this lane only ([8t, 8t + 8)); its other entries were
-  // written by other waves before the barrier above, so stage 5's first write is safe.
   head_stages<5, TLOG>(lds, t, v);
   store_eight<TLOG == 13>(lookup + base0, t, v);
 }
