@@ -1251,19 +1251,6 @@ __device__ __forceinline__ void head_stages(uint2* lds, uint32_t t, uint2 (&v)[8
   }
 }
 
-// The bin pass's inputs for a tile (entries q = t + k*NT: a wave's loads and its offsets resets
-// cover consecutive particles): positions, or the previous frame's pad entries [n, P)
-// (the reference never rewrites them).
-template <uint32_t NT>
-__device__ __forceinline__ void bin_load(const uint2* lookup, const SortBin& bin, uint32_t base0, uint32_t t,
-                                         uint2 (&raw)[8]) {
-#pragma unroll
-  for (uint32_t k = 0; k < 8; ++k) {
-    const uint32_t gq = base0 + t + k * NT;
-    raw[k] = gq >= bin.n ? lookup[gq] : bin.prebuilt ? bin.prebuilt[gq] : __builtin_bit_cast(uint2, bin_pos(bin, gq));
-  }
-}
-
 // The bin pass for the eight consecutive entries [g0, g0 + 8): the sim's prebuilt (key, slot)
 // entries and the pad entries [n, P) as four 16-B loads where the eight are all of one kind,
 // positions keyed otherwise; offsets reset as bin_particles_in_grid does (wgsl:467).
@@ -1618,26 +1605,17 @@ template <int TLOG, bool OUT_LOOKUP>
 __global__ __launch_bounds__(1u << (TLOG - 3)) __attribute__((amdgpu_waves_per_eu(4))) void sph_csort_head_kernel(
     uint2* __restrict__ lookup, SortBin bin, uint32_t* __restrict__ cout) {
   static_assert(TLOG >= 11 && TLOG <= 13, "eight entries per thread, 256..1024 threads");
-  constexpr uint32_t TILE = 1u << TLOG, NT = TILE / 8;
+  constexpr uint32_t TILE = 1u << TLOG;
   __shared__ uint32_t lds[TILE + TILE / 32];
   const uint32_t t = threadIdx.x;
   const uint32_t base0 = blockIdx.x * TILE;
-  {
-    uint2 raw[8];
-    bin_load<NT>(lookup, bin, base0, t, raw);
-#pragma unroll
-    for (uint32_t k = 0; k < 8; ++k) {
-      const uint32_t q = t + k * NT, gq = base0 + q;
-      if (gq < bin.n && bin.prebuilt && bin.reset_pre) bin_reset(bin, gq);
-      const uint2 e = (gq >= bin.n || bin.prebuilt) ? raw[k] : bin_key(bin, __builtin_bit_cast(f2, raw[k]), gq);
-      lds[padded(q)] = cpack(e);
-    }
-  }
-  __syncthreads();
   uint32_t v[8];
-  const uint32_t a = padded(8u * t);
+  {
+    uint2 e[8];
+    bin_load_eight(lookup, bin, base0 + 8u * t, e);  // the lane's eight entries, no LDS image
 #pragma unroll
-  for (int i = 0; i < 8; ++i) v[i] = lds[a + i];
+    for (int i = 0; i < 8; ++i) v[i] = cpack(e[i]);
+  }
   ccas4(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);  // stages 0-2 (reg_stages012)
   ccas4(v[0], v[3], v[1], v[2], v[4], v[7], v[5], v[6]);
   ccas4(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
