@@ -3086,6 +3086,10 @@ __global__ __launch_bounds__(kBlock) void sph_runs_kernel(SphLayoutArgs a, const
   const uint32_t u = t + 64u;  // slot lane of the 64 after the wave
   const bool same = u < n && lookup[u].x == klast;
   const uint64_t other = __builtin_amdgcn_ballot_w64(!same);
+  // The payloads of the kRunIdx - 1 slots after this one, from the lanes that loaded them.
+  uint32_t nxt[kRunIdx];
+#pragma unroll
+  for (uint32_t k = 1; k < kRunIdx; ++k) nxt[k] = (uint32_t)__shfl_down((int)e.y, k, 64);
   if (!start) return;
   const uint64_t above = lane == 63u ? 0ull : starts >> (lane + 1u);
   const uint32_t len = above ? (uint32_t)__builtin_ctzll(above) + 1u
@@ -3094,11 +3098,11 @@ __global__ __launch_bounds__(kBlock) void sph_runs_kernel(SphLayoutArgs a, const
   // ops), so its key is e.x; anything else (never seen) is handled as outside the grid.
   const f4 s = st[resolve_payload(e.y, nullptr, bin_prev).state];
   // The first kRunIdx particle indices (the write pass then needs no lookup gathers for
-  // them), loaded together (adjacent, mostly one line).
+  // them): from the wave's lanes, loaded only past the wave's end.
   uint32_t idx[kRunIdx];
   idx[0] = e.y;
 #pragma unroll
-  for (uint32_t k = 1; k < kRunIdx; ++k) idx[k] = k < len ? lookup[t + k].y : 0u;
+  for (uint32_t k = 1; k < kRunIdx; ++k) idx[k] = k >= len ? 0u : lane + k < 64u ? nxt[k] : lookup[t + k].y;
   const float r = cfg->smoothing_radius;
   const int32_t cx = f32_to_i32((s[0] + cfg->screen_bounds[1]) / r);
   const int32_t cy = f32_to_i32((s[1] + cfg->screen_bounds[3]) / r);
