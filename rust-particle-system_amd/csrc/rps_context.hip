@@ -53,7 +53,6 @@ struct rps_ctx {
   uint32_t P = 0;
   uint32_t sort_passes = 0, sort_launches = 0;
   bool sort_fold = true;  // RPS_SPH_SORT_FOLD (rps_kernels.hip, launch_sph_sort)
-  bool sort_win = false;  // RPS_SPH_SORT_WIN (rps_kernels.hip, launch_sph_sort)
   bool csort = true;      // RPS_SPH_CSORT: the compact sort at 2^11 <= P <= 2^16
   uint8_t csort_tlog = 0; // RPS_SPH_CSORT_TLOG (11..13; 0: by size)
   uint8_t csort_wide = 4; // RPS_SPH_CSORT_WIDE
@@ -320,7 +319,6 @@ SphBuffers sph_buffers(rps_ctx* ctx) {
   b.cell_cap = ctx->cell_cap;
   b.layout = ctx->layout_last;
   b.sort_fold = ctx->sort_fold;
-  b.sort_win = ctx->sort_win;
   b.csort = ctx->csort;
   b.csort_tlog = ctx->csort_tlog;
   b.csort_wide = ctx->csort_wide;
@@ -666,7 +664,6 @@ int rps_create(const rps_create_info* info, rps_ctx** out) {
     ctx->P = next_pow2_u32((uint32_t)n);  // spatial lookup sized next_pow2 (particle_buffers.rs:86)
     const size_t P = ctx->P;
     ctx->sort_fold = env_int("RPS_SPH_SORT_FOLD", 1) != 0;
-    ctx->sort_win = env_int("RPS_SPH_SORT_WIN", 0) != 0;
     ctx->csort = env_int("RPS_SPH_CSORT", 1) != 0;
     ctx->csort_tlog = (uint8_t)std::max(0, std::min(13, env_int("RPS_SPH_CSORT_TLOG", 0)));
     ctx->csort_wide = (uint8_t)std::max(0, std::min(5, env_int("RPS_SPH_CSORT_WIDE", 4)));

@@ -184,7 +184,6 @@ struct SphBuffers {
   uint8_t batch_s;   //   0: by size, sph_batch); per context, RPS_SPH_BATCH[_D|_S] at create
   bool layout;       // this frame uses the spatial record layout (lay.* valid)
   bool sort_fold;    // the first two later sort stages fold their global passes into the tails
-  bool sort_win;     // 8192-entry tiles: the later stages as window launches (RPS_SPH_SORT_WIN)
   bool csort;        // 2^11 <= P <= 2^16: the compact (4-byte entry) sort, RPS_SPH_CSORT
   uint8_t csort_tlog;  // its tile (11..13; 0: by size), RPS_SPH_CSORT_TLOG
   uint8_t csort_wide;  // its stages of this many folded passes or more fold with twice the threads (0: none), RPS_SPH_CSORT_WIDE

@@ -8,7 +8,6 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
-#include <vector>
 
 #include "rps_internal.hpp"
 
@@ -1405,160 +1404,6 @@ __global__ __launch_bounds__(1u << (T + LW + 1 - LE)) __attribute__((amdgpu_wave
   gather_mid_chunks<TL - LE, LW + 1, LE>(lds, t);  // strides gp/2 .. 2W, all but the last chunk
   constexpr int KL = T + 1 - LE >= LE ? LE : T + 1 - LE;
   lds_chunk_out<LW + KL, KL, LE>(lds, t, [&](uint32_t tau, uint2 e) { lookup[pos(tau)] = e; });
-}
-
-// ---------------------------------------------------------------------------------------
-// Window launches (8192-entry groups, P >= 2^21): the passes after the head cut into windows of
-// consecutive passes that cross stage boundaries -- a stage's last in-tile passes together with
-// the next stage's flip and first global passes -- instead of one global launch and one tail per
-// stage (2^22: 14 launches instead of 18).  A window's distinct pass masks (2^b, or the flip's
-// 2^(s+1) - 1) are independent, so the positions x0 ^ (xor of any subset of them) form a group
-// of 2^13 entries closed under every pass of the window (with position bits 0-3 always in it:
-// whole 128-B lines); in local coordinates c (13 bits, local bit i <-> mask[i]) every pass is an
-// exchange of one local bit, and its lower position is the entry whose position bit (the mask's
-// top bit) is 0: c's bit, complemented by the flip's local bit for passes below the flip (every
-// pass of a window with a flip but the flip itself; win_passes).  The host builds each window
-// (sort_windows); tests/test_sort_schedule.py replays it.
-struct SortWindow {
-  uint32_t mask[13];  // local bit i -> position xor mask
-  uint32_t coset;     // position bits outside the group: x0 = the block index deposited there
-  uint32_t fbit;      // local bit of the window's flip (31: none)
-  uint32_t nch;       // register chunks (up to three passes each)
-  uint32_t direct;    // bit 0: chunk 0 runs on the loaded registers (local bits 10-12); bit 1: the
-                      //   last chunk's registers (local bits 7-9) are stored
-  uint32_t chunk[8];  // per register chunk, 4-bit fields: register bits rb0-rb2 (pass q exchanges
-                      //   rb_q), the same ascending rs0-rs2, passes (bits 24-25), bit 27 + q: pass
-                      //   q is the flip
-};
-__host__ __device__ constexpr uint32_t win_field(uint32_t ch, int k) { return (ch >> (4 * k)) & 15u; }
-constexpr uint32_t kWinMaxChunks = 8;
-
-// The flip pass (a: the entry with the flip's local bit 0, b: its partner, whose key is held
-// complemented): swap when a's key exceeds b's, each moved key re-complemented.
-__device__ __forceinline__ void cas_flip(uint2& a, uint2& b) {
-  const uint64_t m = __builtin_amdgcn_ballot_w64(a.x > ~b.x);
-  uint64_t sv;
-  asm volatile("s_mov_b64 %[sv], exec\n\t"
-               "s_mov_b64 exec, %[m]\n\t"
-               "v_not_b32 %[ax], %[ax]\n\t"
-               "v_not_b32 %[bx], %[bx]\n\t"
-               "v_swap_b32 %[ax], %[bx]\n\t"
-               "v_swap_b32 %[ay], %[by]\n\t"
-               "s_mov_b64 exec, %[sv]"
-               : [ax] "+v"(a.x), [bx] "+v"(b.x), [ay] "+v"(a.y), [by] "+v"(b.y), [sv] "=&s"(sv)
-               : [m] "s"(m));
-}
-
-// The chunk's passes on the eight registers (pass q pairs k, k | 2^q).  Keys of entries whose
-// flip bit is 1 are held complemented (win_key), so every pass below the flip, whose lower
-// position there is the entry with the local bit 1, is a plain compare-swap; only the flip pass
-// itself (bit q of `flips`) compares across the two halves.
-template <int Q>
-__device__ __forceinline__ void win_pass(uint2 (&v)[8], bool flip) {
-  constexpr int d = 1 << Q;
-  constexpr int j0 = pair_lo(0, Q), j1 = pair_lo(1, Q), j2 = pair_lo(2, Q), j3 = pair_lo(3, Q);
-  if (flip) {
-    cas_flip(v[j0], v[j0 + d]);
-    cas_flip(v[j1], v[j1 + d]);
-    cas_flip(v[j2], v[j2 + d]);
-    cas_flip(v[j3], v[j3 + d]);
-  } else {
-    cas4(v[j0], v[j0 + d], v[j1], v[j1 + d], v[j2], v[j2 + d], v[j3], v[j3 + d]);
-  }
-}
-__device__ __forceinline__ void win_passes(uint2 (&v)[8], uint32_t np, uint32_t flips) {
-  win_pass<0>(v, flips & 1u);
-  if (np > 1u) win_pass<1>(v, (flips >> 1) & 1u);
-  if (np > 2u) win_pass<2>(v, (flips >> 2) & 1u);
-}
-// A key as held in LDS and registers: complemented where the entry's flip bit is 1.
-__device__ __forceinline__ void win_key(uint2& e, uint32_t c, uint32_t fbit) { e.x ^= 0u - ((c >> fbit) & 1u); }
-
-__device__ __forceinline__ uint32_t insert_zero(uint32_t x, uint32_t p) {
-  return ((x >> p) << (p + 1u)) | (x & ((1u << p) - 1u));
-}
-
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4))) void sph_sort_window_kernel(
-    uint2* __restrict__ lookup, SortWindow w) {
-  constexpr uint32_t G = 1u << 13;
-  __shared__ uint2 lds[G + G / 32];
-  const uint32_t t = threadIdx.x;
-  uint32_t x0 = 0;
-  {  // the block index deposited into the coset bits (uniform)
-    uint32_t b = blockIdx.x;
-    for (uint32_t m = w.coset; m; m &= m - 1u, b >>= 1)
-      if (b & 1u) x0 |= m & (0u - m);
-  }
-  const auto position = [&](uint32_t c) {
-    uint32_t x = x0;
-#pragma unroll
-    for (int i = 0; i < 13; ++i)
-      if ((c >> i) & 1u) x ^= w.mask[i];
-    return x;
-  };
-  uint2 v[8];
-  uint32_t c[8];
-  {  // load: c = t + 1024 j (lanes on local bits 0-5: whole lines)
-    const uint32_t at = position(t);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      c[j] = t | ((uint32_t)j << 10);
-      v[j] = lookup[at ^ position((uint32_t)j << 10) ^ x0];
-      win_key(v[j], c[j], w.fbit);
-    }
-    if (w.direct & 1u) win_passes(v, (w.chunk[0] >> 24) & 3u, w.chunk[0] >> 27);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) lds[padded(c[j])] = v[j];
-  }
-  __syncthreads();
-  const uint32_t ch_beg = w.direct & 1u, ch_end = w.nch - ((w.direct >> 1) & 1u);
-#pragma unroll
-  for (uint32_t ch = 0; ch < kWinMaxChunks; ++ch) {  // compile-time chunk index: scalar parameter loads
-    if (ch < ch_beg || ch >= ch_end) continue;
-    const uint32_t cw = w.chunk[ch];
-    const uint32_t b0 = win_field(cw, 0), b1 = win_field(cw, 1), b2 = win_field(cw, 2);
-    const uint32_t base = insert_zero(insert_zero(insert_zero(t, win_field(cw, 3)), win_field(cw, 4)), win_field(cw, 5));
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      c[k] = base | ((uint32_t)(k & 1) << b0) | ((uint32_t)((k >> 1) & 1) << b1) | ((uint32_t)(k >> 2) << b2);
-      v[k] = lds[padded(c[k])];
-    }
-    win_passes(v, (cw >> 24) & 3u, cw >> 27);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) lds[padded(c[k])] = v[k];
-    __syncthreads();
-  }
-  if (w.direct & 2u) {  // the last chunk on local bits 7-9, stored from its registers
-    const uint32_t ch = w.nch - 1u;  // its parameters by a uniform select (no dynamic kernarg index)
-    uint32_t cw = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < kWinMaxChunks; ++k)
-      if (k == ch) cw = w.chunk[k];
-    const uint32_t base = (t & 127u) | ((t >> 7) << 10);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      c[k] = base | ((uint32_t)k << 7);
-      v[k] = lds[padded(c[k])];
-    }
-    win_passes(v, (cw >> 24) & 3u, cw >> 27);
-    const uint32_t at = position(base);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) win_key(v[k], c[k], w.fbit);
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      __builtin_nontemporal_store(__builtin_bit_cast(uint64_t, v[k]),
-                                  reinterpret_cast<uint64_t*>(lookup + (at ^ position((uint32_t)k << 7) ^ x0)));
-  } else {
-    const uint32_t at = position(t);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint32_t cj = t | ((uint32_t)j << 10);
-      uint2 e = lds[padded(cj)];
-      win_key(e, cj, w.fbit);
-      __builtin_nontemporal_store(__builtin_bit_cast(uint64_t, e),
-                                  reinterpret_cast<uint64_t*>(lookup + (at ^ position((uint32_t)j << 10) ^ x0)));
-    }
-  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -3685,132 +3530,6 @@ static bool csort_ok(const SphBuffers& b) {
 }
 
 // Passes 1-2 of the frame: bin (folded into the first sort launch) + the bitonic network.
-// The window schedule of the passes after an 8192-entry head (sph_sort_window_kernel): greedy
-// windows of consecutive passes with at most 13 local bits (distinct masks plus the position
-// bits 0-3 not among them), distinct top bits and at most one flip; mirrored by
-// tests/test_sort_schedule.py (sort_windows).
-struct WinMask {
-  bool flip;
-  uint32_t bit;  // the mask's top bit
-  bool operator==(const WinMask& o) const { return flip == o.flip && bit == o.bit; }
-};
-static std::vector<SortWindow> sort_windows(uint32_t stages) {
-  constexpr uint32_t L = 13, LB = 4;
-  std::vector<WinMask> seq;
-  for (uint32_t st = L; st < stages; ++st) {
-    seq.push_back({true, st});
-    for (int b = (int)st - 1; b >= 0; --b) seq.push_back({false, (uint32_t)b});
-  }
-  const auto cost = [&](const std::vector<WinMask>& m) {
-    uint32_t low = 0;
-    for (const WinMask& x : m)
-      if (x.bit < LB) low |= 1u << x.bit;
-    return (uint32_t)m.size() + (LB - (uint32_t)__builtin_popcount(low));
-  };
-  const auto has = [](const std::vector<WinMask>& v, const WinMask& m) {
-    return std::find(v.begin(), v.end(), m) != v.end();
-  };
-  std::vector<SortWindow> out;
-  size_t i = 0;
-  while (i < seq.size()) {
-    std::vector<WinMask> masks;
-    size_t j = i;
-    for (; j < seq.size(); ++j) {
-      const WinMask m = seq[j];
-      if (has(masks, m)) continue;
-      bool clash = false, flip = false;
-      for (const WinMask& x : masks) {
-        clash |= x.bit == m.bit;
-        flip |= x.flip;
-      }
-      std::vector<WinMask> with = masks;
-      with.push_back(m);
-      if (clash || cost(with) > L || (m.flip && flip)) break;
-      masks = with;
-    }
-    const std::vector<WinMask> win(seq.begin() + (long)i, seq.begin() + (long)j);
-    i = j;
-    const uint32_t n = (uint32_t)win.size();
-    SortWindow w{};
-    // direct chunks: the first / last (up to three) passes above the line bits, distinct
-    uint32_t f = 0, l = 0;
-    while (f < std::min(3u, n) && win[f].bit >= LB && !has({win.begin(), win.begin() + f}, win[f])) ++f;
-    while (l < std::min(3u, n - f) && win[n - 1 - l].bit >= LB &&
-           !has({win.end() - (long)l, win.end()}, win[n - 1 - l]))
-      ++l;
-    // local bits: 0-3 the line bits, 10-12 the first chunk's, 7-9 the last chunk's, then the rest
-    int local_of[2][32];
-    std::fill(&local_of[0][0], &local_of[0][0] + 64, -1);
-    bool used[L] = {};
-    for (uint32_t b = 0; b < LB; ++b) used[b] = true;
-    for (uint32_t q = 0; q < f; ++q) local_of[win[q].flip][win[q].bit] = 10 + (int)q, used[10 + q] = true;
-    for (uint32_t q = 0; q < l; ++q) {
-      const WinMask& m = win[n - l + q];
-      local_of[m.flip][m.bit] = 7 + (int)q, used[7 + q] = true;
-    }
-    uint32_t pos_used = (1u << LB) - 1u;  // position bits inside the group
-    for (const WinMask& m : masks) {
-      pos_used |= 1u << m.bit;
-      if (!m.flip && m.bit < LB) local_of[0][m.bit] = (int)m.bit;
-    }
-    int fbit = 31;
-    for (const WinMask& m : masks) {
-      int& lb = local_of[m.flip][m.bit];
-      if (lb < 0) {
-        uint32_t k = LB;
-        while (used[k]) ++k;
-        lb = (int)k, used[k] = true;
-      }
-      w.mask[lb] = m.flip ? (2u << m.bit) - 1u : 1u << m.bit;
-      if (m.flip) fbit = lb;
-    }
-    for (uint32_t b = 0; b < LB; ++b) w.mask[b] = 1u << b;
-    for (uint32_t k = LB, p = LB; k < L; ++k) {  // unused local bits: the lowest free position bits
-      if (used[k]) continue;
-      while (pos_used >> p & 1u) ++p;
-      w.mask[k] = 1u << p, pos_used |= 1u << p;
-    }
-    w.coset = ((stages >= 32 ? 0u : (1u << stages)) - 1u) & ~pos_used;
-    w.fbit = (uint32_t)fbit;
-    const uint32_t flip_top = fbit == 31 ? 0u : 31u - (uint32_t)__builtin_clz(w.mask[fbit]);
-    std::vector<uint32_t> pb(n);
-    for (uint32_t q = 0; q < n; ++q) {
-      pb[q] = (uint32_t)local_of[win[q].flip][win[q].bit];
-      // win_passes: with a flip, every other pass lies below it (held as complemented keys)
-      if (fbit != 31 && !win[q].flip && win[q].bit >= flip_top) abort();
-    }
-    const auto add_chunk = [&](uint32_t q0, uint32_t np, const uint32_t* rb) {
-      if (w.nch >= kWinMaxChunks) abort();
-      const uint32_t ch = w.nch++;
-      uint32_t r[3] = {rb[0], rb[1], rb[2]};
-      std::sort(r, r + 3);
-      uint32_t cw = rb[0] | rb[1] << 4 | rb[2] << 8 | r[0] << 12 | r[1] << 16 | r[2] << 20 | np << 24;
-      for (uint32_t q = 0; q < np; ++q) cw |= (uint32_t)win[q0 + q].flip << (27 + q);
-      w.chunk[ch] = cw;
-    };
-    if (f) {
-      const uint32_t rb[3] = {10, 11, 12};
-      add_chunk(0, f, rb);
-      w.direct |= 1u;
-    }
-    for (uint32_t q = f; q < n - l;) {
-      uint32_t rb[3], k = 0;
-      while (k < 3 && q + k < n - l && std::find(rb, rb + k, pb[q + k]) == rb + k) rb[k] = pb[q + k], ++k;
-      for (int b = (int)L - 1, m = (int)k; m < 3; --b)  // fillers: the highest other local bits
-        if (std::find(rb, rb + m, (uint32_t)b) == rb + m) rb[m++] = (uint32_t)b;
-      add_chunk(q, k, rb);
-      q += k;
-    }
-    if (l) {
-      const uint32_t rb[3] = {7, 8, 9};
-      add_chunk(n - l, l, rb);
-      w.direct |= 2u;
-    }
-    out.push_back(w);
-  }
-  return out;
-}
-
 hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
                            uint32_t* launches) {
   const uint32_t P = b.p;
@@ -3853,15 +3572,6 @@ hipError_t launch_sph_sort(const SphBuffers& b, hipStream_t s, uint32_t* passes,
   e = hipGetLastError();
   ++*launches;
   if (e != hipSuccess) return e;
-  if (b.sort_win && tile_log == 13u) {  // the later stages as window launches
-    for (const SortWindow& w : sort_windows(stages)) {
-      hipLaunchKernelGGL(sph_sort_window_kernel, dim3(P >> 13), dim3(1024), 0, s, b.lookup, w);
-      e = hipGetLastError();
-      ++*launches;
-      if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
-  }
   // The first two later stages (one and two global passes) fold those passes into their tail
   // launches, which then read one buffer and write the other (the neighbour masks' buffer,
   // dead during the sort): lookup -> scratch -> lookup.  Tiles up to 4096 entries (same box,

@@ -588,120 +588,3 @@ def test_compact_entries_fit():
     p = g.integers(0, 1 << 16, (1000, 2)).astype(np.uint32)
     packed = (k << np.uint32(16)) | p
     np.testing.assert_array_equal((packed[:, 0] >> 16) > (packed[:, 1] >> 16), k[:, 0] > k[:, 1])
-
-
-# Window launches (sph_sort_window_kernel, sort_windows in rps_kernels.hip): the passes after an
-# 8192-entry head in greedy windows of at most 13 local bits.
-WIN_L, WIN_LB = 13, 4
-
-
-def sort_windows(stages):
-    """sort_windows: per window its masks (local bit -> position xor mask), coset bits, flip's
-    local bit, chunks (register bits, passes, dep bits) and direct flags."""
-    seq = []
-    for st in range(WIN_L, stages):
-        seq.append((True, st))
-        seq += [(False, b) for b in range(st - 1, -1, -1)]
-
-    def cost(m):
-        return len(m) + WIN_LB - len({b for _, b in m if b < WIN_LB})
-
-    out, i = [], 0
-    while i < len(seq):
-        masks, j = [], i
-        while j < len(seq):
-            m = seq[j]
-            if m not in masks:
-                if any(b == m[1] for _, b in masks) or cost(masks + [m]) > WIN_L or (m[0] and any(f for f, _ in masks)):
-                    break
-                masks.append(m)
-            j += 1
-        win, i = seq[i:j], j
-        n = len(win)
-        f = 0
-        while f < min(3, n) and win[f][1] >= WIN_LB and win[f] not in win[:f]:
-            f += 1
-        l = 0
-        while l < min(3, n - f) and win[n - 1 - l][1] >= WIN_LB and win[n - 1 - l] not in win[n - l:]:
-            l += 1
-        local = {m: 10 + q for q, m in enumerate(win[:f])}
-        local.update({m: 7 + q for q, m in enumerate(win[n - l:])})
-        pos_used = set(range(WIN_LB)) | {b for _, b in masks}
-        local.update({m: m[1] for m in masks if not m[0] and m[1] < WIN_LB})
-        mask = [1 << b if b < WIN_LB else None for b in range(WIN_L)]
-        for m in masks:
-            if m not in local:
-                local[m] = min(k for k in range(WIN_LB, WIN_L) if k not in local.values())
-            mask[local[m]] = (2 << m[1]) - 1 if m[0] else 1 << m[1]
-        for k in range(WIN_LB, WIN_L):
-            if mask[k] is None and k not in local.values():
-                p = min(p for p in range(WIN_LB, 32) if p not in pos_used)
-                mask[k] = 1 << p
-                pos_used.add(p)
-        flip = [m for m in masks if m[0]]
-        fbit = local[flip[0]] if flip else 31
-        pb = [local[m] for m in win]
-        dep = [bool(flip) and not m[0] and m[1] < flip[0][1] for m in win]
-        chunks = []
-        if f:
-            chunks.append(([10, 11, 12], list(range(f))))
-        q = f
-        while q < n - l:
-            k = []
-            while len(k) < 3 and q + len(k) < n - l and pb[q + len(k)] not in [pb[x] for x in k]:
-                k.append(q + len(k))
-            rb = [pb[x] for x in k]
-            rb += [b for b in range(WIN_L - 1, -1, -1) if b not in rb][:3 - len(rb)]
-            chunks.append((rb, k))
-            q += len(k)
-        if l:
-            chunks.append(([7, 8, 9], list(range(n - l, n))))
-        coset = [p for p in range(stages) if p not in pos_used]
-        out.append(dict(mask=mask, coset=coset, fbit=fbit, pb=pb, dep=dep, chunks=chunks,
-                        direct=(f > 0, l > 0)))
-    return out
-
-
-def window_launch(a, w):
-    """sph_sort_window_kernel over every workgroup: the group's entries at x0 ^ (masks of c's
-    bits), then each chunk's passes on local bits (the lower entry: c's bit, complemented by the
-    flip's local bit for `dep` passes)."""
-    a = a.copy()
-    c = np.arange(1 << WIN_L)
-    for blk in range(len(a) >> WIN_L):
-        x0 = sum(1 << p for i, p in enumerate(w['coset']) if (blk >> i) & 1)
-        pos = np.full(1 << WIN_L, x0)
-        for i in range(WIN_L):
-            pos = np.where((c >> i) & 1, pos ^ w['mask'][i], pos)
-        assert len(np.unique(pos)) == 1 << WIN_L
-        g = a[pos].copy()
-        for rb, idx in w['chunks']:
-            assert len(set(rb)) == 3 and all(w['pb'][x] == rb[q] for q, x in enumerate(idx))
-            for x in idx:
-                b = w['pb'][x]
-                lo = c[(c >> b) & 1 == 0]
-                hi = lo | (1 << b)
-                rev = ((lo >> w['fbit']) & 1).astype(bool) if w['dep'][x] else np.zeros(len(lo), bool)
-                left, right = np.where(rev, hi, lo), np.where(rev, lo, hi)
-                sw = g[left, 0] > g[right, 0]
-                l, r = g[left[sw]].copy(), g[right[sw]].copy()
-                g[left[sw]], g[right[sw]] = r, l
-        a[pos] = g
-    return a
-
-
-@pytest.mark.parametrize("stages", [14, 15, 16, 17])
-@pytest.mark.parametrize("kmax", [5, 1 << 20])
-def test_window_schedule_equals_network(stages, kmax):
-    """The window launches after the 8192-entry head equal the reference's stages 13 .. stages-1,
-    ties included."""
-    keys = np.random.default_rng(stages * 3 + (kmax & 7)).integers(0, kmax, 1 << stages)
-    a = ref_network(keys, 13)
-    for w in sort_windows(stages):
-        a = window_launch(a, w)
-    np.testing.assert_array_equal(a, ref_network(keys, stages))
-
-
-def test_window_counts():
-    """Launches after the head: windows vs one global launch (or more) and one tail per stage."""
-    assert [len(sort_windows(s)) for s in (21, 22, 23)] == [12, 14, 17]
