@@ -85,6 +85,10 @@ def parse():
                          "DESIGN.md §6)")
     ap.add_argument("--export-reps", type=int, default=20,
                     help="render-interop export (rps_export_particles) repetitions timed on the headline state; 0: skip")
+    ap.add_argument("--fuse-k", type=int, default=16,
+                    help="temporal fusion side measure on the headline context after its timed region: "
+                         "ext.fuse_steps = K steps per launch (0/1: skip)")
+    ap.add_argument("--fuse-steps", type=int, default=64, help="steps timed with --fuse-k (a multiple of K)")
     ap.add_argument("--export-after", action="store_true",
                     help="measure the export after the headline's timed region instead of before its warmup")
     ap.add_argument("--allpairs-timeout", type=float, default=300.0,
@@ -541,6 +545,31 @@ def sph_cpu_baseline(rps, args):
                       f"-O3 -fopenmp, {threads} threads), {el:.1f} s; {el * 1e3 / args.sph_cpu_frames:.0f} ms/frame"}
 
 
+def fused_side(ctx, d, cfg, ext, n_global, k, steps):
+    """ext.fuse_steps = k (include/rps.h) on the headline's context once its timed region, stats and
+    export are done: k steps per launch with the state in registers, bitwise == k separate steps
+    (tests/test_gpu_stream.py).  Reported beside the headline, not as it: the reference renders
+    between frames (one dispatch per frame), so the headline keeps one launch per step."""
+    import copy
+
+    fext = copy.copy(ext)
+    fext.fuse_steps = k
+    ctx.set_config(cfg, fext)
+    steps = max(k, steps - steps % k)
+    ctx.step(k)  # warm: one fused launch
+    ctx.sync()
+    d.sync_device()
+    d.barrier()
+    ms = d.max(ctx.time_steps(steps))
+    moved, _ = ctx.step_cost()
+    return {"fuse_steps": k, "steps": steps, "launches": steps // k, "ms_per_step": ms / steps,
+            "updates_per_s": float(n_global) * steps / (ms * 1e-3),
+            "moved_bytes_per_step": d.max(moved) / k if moved else None,
+            "timing": "one HIP event pair on the context stream around the fused launches; max over ranks",
+            "note": "opt-in temporal fusion (ext.fuse_steps): each particle read and written once per k steps, "
+                    "so the step is VALU-bound (attractor force), not HBM-bound; headless use only"}
+
+
 def export_side(ctx, n, reps):
     """SURVEY 8(f)3, render interop: rps_export_particles writes the headline state as the
     reference's 32-B Particle buffer (render_shader.wgsl:26-30; colour derived, set_color)
@@ -700,6 +729,10 @@ def main():
     stats["when"] = ("timed region" if stats["step"] >= first_timed else
                      f"warm-up step {stats['step']} (no stats step among the timed steps "
                      f"{first_timed}..{first_timed + args.steps - 1})")
+    fused = None
+    if args.fuse_k > 1:
+        progress(d, f"fused: ext.fuse_steps = {args.fuse_k}")
+        fused = fused_side(ctx, d, cfg, ext, n_global, args.fuse_k, args.fuse_steps)
     ctx.close()
 
     updates = float(n_global) * args.steps
@@ -756,6 +789,8 @@ def main():
     line["roofline"]["infinity_cache_resident"] = state_bytes <= 256 * 1024 * 1024
     if export is not None:
         line["export"] = export
+    if fused is not None:
+        line["fused"] = fused
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
         progress(d, "cpu_baseline")
         line["cpu_baseline"] = cpu_baseline(rps, args, cfg, ext)
