@@ -2316,9 +2316,8 @@ __global__ __launch_bounds__(kBlock) void sph_density2_kernel(const rps_config* 
 }
 
 // A long scan of the density pass (kLongScan): one queued slot per wave, 64 entries per step.
-template <bool LAYOUT>
 __global__ __launch_bounds__(kBlock) void sph_density_long_kernel(const rps_config* __restrict__ cfg,
-                                                                  RunBounds rb, SphSlots sl, uint32_t p_slots) {
+                                                                  SphSlots sl, uint32_t p_slots) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // uniform: the queue entry and its table go to SGPRs
   const uint32_t nw = gridDim.x * (kBlock / 64u);
@@ -2770,8 +2769,7 @@ __global__ __launch_bounds__(kBlock) void sph_sim2_kernel(const rps_config* __re
 // (long_compact, then every lane reads them back in order).
 typedef f4 LongTerms[kBlock / 64u][64u * kLongSub];  // 16 KiB: fits a RunTable's 18 KiB
 template <bool kPads, bool LAYOUT>
-__device__ __forceinline__ void sim_long_body(const rps_config* __restrict__ cfg, const RunBounds& rb,
-                                              const SphSlots& sl, f4* __restrict__ st, uint2* __restrict__ bin_next,
+__device__ __forceinline__ void sim_long_body(const rps_config* __restrict__ cfg, const SphSlots& sl, f4* __restrict__ st, uint2* __restrict__ bin_next,
                                               uint32_t bid, uint32_t nblk, LongTerms& terms) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // uniform: the queue entry and its table go to SGPRs
@@ -2868,10 +2866,10 @@ __device__ __forceinline__ void sim_long_body(const rps_config* __restrict__ cfg
 
 template <bool kPads, bool LAYOUT>
 __global__ __launch_bounds__(kBlock) void sph_sim_long_kernel(const rps_config* __restrict__ cfg,
-                                                              RunBounds rb, SphSlots sl, f4* __restrict__ st,
+                                                              SphSlots sl, f4* __restrict__ st,
                                                               uint2* __restrict__ bin_next) {
   __shared__ LongTerms terms;
-  sim_long_body<kPads, LAYOUT>(cfg, rb, sl, st, bin_next, blockIdx.x, gridDim.x, terms);
+  sim_long_body<kPads, LAYOUT>(cfg, sl, st, bin_next, blockIdx.x, gridDim.x, terms);
 }
 
 // The sim pass in one launch with the long scans (P != N): blocks [0, nlong) take the queued
@@ -2886,7 +2884,7 @@ __global__ __launch_bounds__(kBlock) void sph_sim_fused_kernel(const rps_config*
                                                                uint32_t nlong) {
   __shared__ RunTable runs;
   if (blockIdx.x < nlong) {
-    sim_long_body<kPads, LAYOUT>(cfg, rb, sl, st, bin_next, blockIdx.x, nlong, reinterpret_cast<LongTerms&>(runs));
+    sim_long_body<kPads, LAYOUT>(cfg, sl, st, bin_next, blockIdx.x, nlong, reinterpret_cast<LongTerms&>(runs));
     return;
   }
   if constexpr (G > 1) sim2_body<kScanBatch, kPads, LAYOUT, G>(cfg, rb, sl, st, bin_next, p_slots, blockIdx.x - nlong, runs);
@@ -3717,10 +3715,7 @@ static hipError_t launch_sph_density(const SphBuffers& b, hipStream_t s) {
   if (b.sl.longq) {
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    if (b.layout)
-      hipLaunchKernelGGL((sph_density_long_kernel<true>), dim3(long_blocks(b.p)), dim3(kBlock), 0, s, b.cfg, rb, b.sl, b.p);
-    else
-      hipLaunchKernelGGL((sph_density_long_kernel<false>), dim3(long_blocks(b.p)), dim3(kBlock), 0, s, b.cfg, rb, b.sl, b.p);
+    hipLaunchKernelGGL(sph_density_long_kernel, dim3(long_blocks(b.p)), dim3(kBlock), 0, s, b.cfg, b.sl, b.p);
   }
   return hipGetLastError();
 }
@@ -3853,11 +3848,11 @@ hipError_t launch_sph_sim(const SphBuffers& b, hipStream_t s) {
     if (e != hipSuccess) return e;
     const dim3 g(long_blocks(b.p));
     if (b.layout)  // long scans exist only with P != N
-      hipLaunchKernelGGL((sph_sim_long_kernel<true, true>), g, dim3(kBlock), 0, s, b.cfg, rb, b.sl, b.st, b.bin_next);
+      hipLaunchKernelGGL((sph_sim_long_kernel<true, true>), g, dim3(kBlock), 0, s, b.cfg, b.sl, b.st, b.bin_next);
     else if (b.p == b.n)
-      hipLaunchKernelGGL((sph_sim_long_kernel<false, false>), g, dim3(kBlock), 0, s, b.cfg, rb, b.sl, b.st, b.bin_next);
+      hipLaunchKernelGGL((sph_sim_long_kernel<false, false>), g, dim3(kBlock), 0, s, b.cfg, b.sl, b.st, b.bin_next);
     else
-      hipLaunchKernelGGL((sph_sim_long_kernel<true, false>), g, dim3(kBlock), 0, s, b.cfg, rb, b.sl, b.st, b.bin_next);
+      hipLaunchKernelGGL((sph_sim_long_kernel<true, false>), g, dim3(kBlock), 0, s, b.cfg, b.sl, b.st, b.bin_next);
   }
   return hipGetLastError();
 }
