@@ -67,6 +67,23 @@ def test_single_process_defaults_to_one_gpu():
 
 
 @pytest.mark.parametrize("gpus", [1, 2])
+def test_fused_side_beside_the_headline(gpus):
+    """The temporally fused measure (ext.fuse_steps = 16) rides on the headline context after its
+    timed region: its steps round to whole launches and its rate counts every rank's particles
+    (the stub times 0.5 ms per step); --fuse-k 0 drops it."""
+    p, lines = _run(WEAK + ["--gpus", str(gpus), "--allpairs-n", "0", "--fuse-steps", "70"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    f = lines[0]["fused"]
+    assert f["fuse_steps"] == 16 and f["steps"] == 64 and f["launches"] == 4
+    assert f["ms_per_step"] == pytest.approx(0.5)
+    assert f["updates_per_s"] == pytest.approx(gpus * 4096 * 64 / (0.5 * 64 * 1e-3))
+    assert lines[0]["value"] > 0 and "fused" not in lines[0]["config"]
+    p, lines = _run(WEAK + ["--allpairs-n", "0", "--fuse-k", "0"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert "fused" not in lines[0]
+
+
+@pytest.mark.parametrize("gpus", [1, 2])
 def test_strong_default_is_the_metric_config(gpus):
     """Without --particles the headline is BASELINE's metric configuration at every N: 1e8
     particles in all, split into contiguous shards; value counts the global particles."""
